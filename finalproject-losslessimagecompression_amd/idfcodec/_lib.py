@@ -1,0 +1,136 @@
+"""ctypes binding of libidfcodec.so (the C ABI declared in include/idf_codec.h).
+
+torch is imported first so that the HIP runtime torch ships (soname
+libamdhip64.so.7) is the one libidfcodec.so binds to: device pointers and
+stream handles from torch are then valid in the library.
+
+There is no fallback: if the library is missing or no GPU is visible, compute
+entry points raise.  Tests on CPU only load the library and inspect exports.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module doc)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+REPO = os.path.dirname(PKG)
+LIB_PATH = os.path.join(HERE, "libidfcodec.so")
+HEADER = os.path.join(REPO, "include", "idf_codec.h")
+
+IDF_OK = 0
+ERR_NAMES = {1: "IDF_ERR_ARG", 2: "IDF_ERR_HIP", 3: "IDF_ERR_WORKSPACE", 4: "IDF_ERR_UNSUPPORTED"}
+
+STREAM_SCALE_ZERO = 1
+STREAM_FREQ_ZERO = 2
+STREAM_NEG_CDF = 4
+STREAM_UNDERFLOW = 8
+STREAM_OUT_OF_WINDOW = 16
+STREAM_WORDS_LEFT = 32
+
+ACT = {"ReLU": 0, "LeakyReLU": 1, "Tanh": 2, "None": 3}
+TAG_CONV1X1, TAG_CONV3X3, TAG_HEAD = 0, 1, 2
+EPI_STORE, EPI_COUPLE_ADD, EPI_COUPLE_SUB, EPI_PRIOR = 0, 1, 2, 3
+MAX_DEPTH = 32
+
+P = ctypes.c_void_p
+i32 = ctypes.c_int32
+i64 = ctypes.c_int64
+f32 = ctypes.c_float
+u64 = ctypes.c_uint64
+
+
+class IdfDenseBlock(ctypes.Structure):
+    _fields_ = [
+        ("depth", i32), ("act", i32), ("slope", f32), ("g_pad", i32), ("g_alloc", i32),
+        ("k_in", i32 * (MAX_DEPTH + 1)), ("n1_alloc", i32 * MAX_DEPTH), ("ldw1", i32 * MAX_DEPTH),
+        ("ldw3", i32 * MAX_DEPTH), ("w1", P * MAX_DEPTH), ("b1", P * MAX_DEPTH),
+        ("w3", P * MAX_DEPTH), ("b3", P * MAX_DEPTH), ("n_head", i32), ("nh_alloc", i32),
+        ("ldwh", i32), ("wh", P), ("bh", P),
+        ("c_real", i32 * (MAX_DEPTH + 1)), ("g_real", i32 * MAX_DEPTH),
+    ]
+
+
+class IdfHeadOut(ctypes.Structure):
+    _fields_ = [
+        ("mode", i32), ("out", P), ("ld_out", i64), ("base", P), ("ld_base", i64),
+        ("n_mean", i32), ("mean", P), ("logscale", P), ("scale", P),
+    ]
+
+
+# name -> (restype, argtypes); mirrors include/idf_codec.h exactly
+SIGNATURES = {
+    "idf_version": (ctypes.c_char_p, []),
+    "idf_device_count": (ctypes.c_int, []),
+    "idf_rans_cdf_freq": (ctypes.c_int, [P, i64, P, P, P, P, P]),
+    "idf_rans_encode_workspace_bytes": (i64, [i64]),
+    "idf_rans_encode_streams": (ctypes.c_int, [P, i64, i64, P, P, P, P, P, P, P, P, P, P, i64]),
+    "idf_rans_decode_streams": (ctypes.c_int, [P, i64, P, P, P, P, P, P, P, P, P, P]),
+    "idf_gather_words": (ctypes.c_int, [P, i64, P, P, P, P, P]),
+    "idf_rans_encode": (ctypes.c_int, [P, i64, P, P, P, P, P, P]),
+    "idf_rans_decode": (ctypes.c_int, [P, P, i64, i64, P, P, P, P]),
+    "idf_expf_glibc": (ctypes.c_int, [P, i64, P, P]),
+    "idf_expf_checksum": (ctypes.c_int, [P, u64, u64, P]),
+    "idf_dense_block_f32": (ctypes.c_int, [P, P, i32, i32, i32, P, i64, P, i64, P]),
+    "idf_timer_create": (P, [i32]),
+    "idf_timer_destroy": (None, [P]),
+    "idf_timer_reset": (None, [P]),
+    "idf_timer_summary": (ctypes.c_int, [P, i32, P, P, P]),
+    "idf_dense_block_f32_timed": (ctypes.c_int, [P, P, i32, i32, i32, P, i64, P, i64, P, P]),
+    "idf_conv1x1_f32": (ctypes.c_int, [P, i64, i32, i32, P, i64, P, i32, i32, P, P, i64, i32, i32,
+                                       i32, P]),
+    "idf_conv3x3_f32": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, i32, P, i32, P, i64,
+                                       i32, f32]),
+    "idf_dequant_u8": (ctypes.c_int, [P, i32, i32, i32, i32, P, P, i64]),
+    "idf_quant_u8": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, P]),
+    "idf_squeeze": (ctypes.c_int, [P, i32, i32, i32, i32, i32, P, i64, P, i64]),
+    "idf_unsqueeze": (ctypes.c_int, [P, i32, i32, i32, i32, i32, P, i64, P, i64]),
+    "idf_permute_couple_in": (ctypes.c_int, [P, i64, i32, P, P, i64, P, i64, i32, i32, P, i64]),
+    "idf_copy_cols": (ctypes.c_int, [P, i64, i32, i32, P, i64, P, i64]),
+    "idf_pm_to_nchw": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P]),
+    "idf_nchw_to_pm": (ctypes.c_int, [P, i32, i32, i32, i32, P, P, i64]),
+    "idf_conv4x4s2_f32": (ctypes.c_int, [P, i32, i32, i32, i32, i32, P, i64, P, P, P, i64]),
+}
+
+_lib = None
+
+
+class IdfError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libidfcodec.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise IdfError(f"libidfcodec.so not built ({LIB_PATH}); run __graft_entry__.build()")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = ""):
+    if rc != IDF_OK:
+        raise IdfError(f"{what}: {ERR_NAMES.get(rc, rc)}")
+
+
+def require_device(t: torch.Tensor, what: str = "tensor"):
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        raise IdfError(f"idfcodec: {what} must be a HIP device tensor (no CPU fallback)")
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> int | None:
+    if t is None:
+        return None
+    return t.data_ptr()

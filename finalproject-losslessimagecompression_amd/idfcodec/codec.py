@@ -1,0 +1,204 @@
+"""End-to-end lossless codec on the GPU: uint8 images <-> rANS bitstreams.
+
+encode: dequant (trainer.py:101) -> IDF forward + priors (flows.py:87-116) ->
+        rANS encode of every (image, level) stream (rans.pyx:37-67, the
+        trainer's per-level reset contract trainer.py:310-315, one stream per
+        image) -> word compaction.
+decode: per level, top first: prior -> rANS decode (rans.pyx:69-110) -> flow
+        inverse (flows.py:118-152) -> unsqueeze; then exact re-quantisation.
+
+Streams are ordered level-major, image-minor; stream (l, b) covers the symbols
+latents[l][b].reshape(-1) (NCHW order) exactly as a reference encode() call on
+that slice would, and is bit-identical to it.
+"""
+from __future__ import annotations
+
+import struct
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr
+
+RANS_L = 1 << 32
+MAGIC = b"IDFB"
+VERSION = 1
+
+
+@dataclass
+class Bitstream:
+    """Per-stream final rANS states + word counts + the concatenated words.
+    Tensors live on the device that produced them (or the host after from_bytes)."""
+    n_images: int
+    level_shapes: list            # [(c, h, w)] per level
+    states: torch.Tensor          # int64 view of u64 final states [n_streams]
+    nwords: torch.Tensor          # int64 [n_streams]
+    words: torch.Tensor           # int32 view of u32 words, stream-major, push order
+    status: torch.Tensor | None = None
+    meta: dict = field(default_factory=dict)
+
+    @property
+    def n_streams(self) -> int:
+        return int(self.states.numel())
+
+    def total_words(self) -> int:
+        return int(self.words.numel())
+
+    def bits(self) -> int:
+        """The reference's accounting (trainer.py:326-327): 64 bits of state per
+        stream + 32 bits per word."""
+        return 64 * self.n_streams + 32 * self.total_words()
+
+    def n_subpixels(self) -> int:
+        return self.meta.get("n_subpixels", 0)
+
+    def bpd(self) -> float:
+        n = self.n_subpixels()
+        return self.bits() / n if n else float("nan")
+
+    def word_offsets(self) -> torch.Tensor:
+        off = torch.zeros_like(self.nwords)
+        if self.nwords.numel() > 1:
+            off[1:] = torch.cumsum(self.nwords, 0)[:-1]
+        return off
+
+    # ---- container (the reference has no file format)
+    def to_bytes(self) -> bytes:
+        hdr = struct.pack("<4sHHIII", MAGIC, VERSION, 0, self.n_images, len(self.level_shapes),
+                          self.n_streams)
+        shapes = b"".join(struct.pack("<III", *s) for s in self.level_shapes)
+        meta = struct.pack("<Q", self.n_subpixels())
+        st = self.states.detach().cpu().numpy().astype("<i8").tobytes()
+        nw = self.nwords.detach().cpu().numpy().astype("<u4").tobytes()
+        w = self.words.detach().cpu().numpy().astype("<i4").tobytes()
+        return hdr + shapes + meta + st + nw + w
+
+    @classmethod
+    def from_bytes(cls, buf: bytes, device=None) -> "Bitstream":
+        magic, ver, _flags, n_img, n_lvl, n_str = struct.unpack_from("<4sHHIII", buf, 0)
+        if magic != MAGIC or ver != VERSION:
+            raise ValueError("not an IDF bitstream")
+        o = struct.calcsize("<4sHHIII")
+        shapes = [struct.unpack_from("<III", buf, o + 12 * i) for i in range(n_lvl)]
+        o += 12 * n_lvl
+        (nsub,) = struct.unpack_from("<Q", buf, o)
+        o += 8
+        st = np.frombuffer(buf, "<i8", n_str, o).copy()
+        o += 8 * n_str
+        nw = np.frombuffer(buf, "<u4", n_str, o).astype(np.int64)
+        o += 4 * n_str
+        w = np.frombuffer(buf, "<i4", int(nw.sum()), o).copy()
+        t = lambda a: torch.from_numpy(a).to(device) if device else torch.from_numpy(a)  # noqa: E731
+        return cls(n_img, [tuple(s) for s in shapes], t(st), t(nw), t(w),
+                   meta={"n_subpixels": int(nsub)})
+
+
+class StreamCoder:
+    """Batched rANS over the engine's flat latent layout."""
+
+    def __init__(self, engine):
+        self.engine = engine
+        self._off = {}
+
+    def sym_off(self, B: int) -> torch.Tensor:
+        t = self._off.get(B)
+        if t is None:
+            offs = [0]
+            for L in self.engine.levels:
+                offs += [offs[-1] + L.n_sym * (b + 1) for b in range(B)]
+            t = torch.tensor(offs, dtype=torch.int64, device=self.engine.device)
+            self._off = {B: t}
+        return t
+
+    def encode(self, ws, B: int, compact: bool = True) -> Bitstream:
+        eng = self.engine
+        dev = eng.device
+        s = _lib.stream_ptr(dev)
+        off = self.sym_off(B)
+        ns = off.numel() - 1
+        nsym = B * eng.n_sym_img
+        init = torch.full((ns,), RANS_L, dtype=torch.int64, device=dev)
+        final = torch.empty(ns, dtype=torch.int64, device=dev)
+        nwords = torch.empty(ns, dtype=torch.int64, device=dev)
+        status = torch.empty(ns, dtype=torch.int32, device=dev)
+        scratch = ws.get("words")
+        if scratch is None or scratch.numel() < nsym:
+            scratch = ws["words"] = torch.empty(nsym, dtype=torch.int32, device=dev)
+        wbytes = lib().idf_rans_encode_workspace_bytes(nsym)
+        wsp = ws.get("rans_ws")
+        if wsp is None or wsp.numel() < wbytes:
+            wsp = ws["rans_ws"] = torch.empty(wbytes, dtype=torch.uint8, device=dev)
+        check(lib().idf_rans_encode_streams(s, ns, nsym, ptr(off), ptr(ws["lat"]), ptr(ws["mean"]),
+                                            ptr(ws["scale"]), ptr(init), ptr(final), ptr(scratch),
+                                            ptr(nwords), ptr(status), ptr(wsp), wbytes),
+              "rans encode")
+        shapes = [(L.z, L.h, L.w) for L in eng.levels]
+        meta = {"n_subpixels": B * eng.C * eng.H * eng.W}
+        if not compact:
+            return Bitstream(B, shapes, final, nwords, scratch, status,
+                             meta=dict(meta, scratch_offsets=off[:-1]))
+        dst_off = torch.zeros_like(nwords)
+        dst_off[1:] = torch.cumsum(nwords, 0)[:-1]
+        total = int((dst_off[-1] + nwords[-1]).item())
+        words = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
+        check(lib().idf_gather_words(s, ns, ptr(off), ptr(nwords), ptr(dst_off), ptr(scratch),
+                                     ptr(words)), "gather words")
+        return Bitstream(B, shapes, final, nwords, words[:total], status, meta=meta)
+
+    def decode_level(self, bs: Bitstream, B: int, l: int, ws, word_off, out_state, out_status):
+        eng = self.engine
+        s = _lib.stream_ptr(eng.device)
+        off = self.sym_off(B)
+        k0, k1 = l * B, (l + 1) * B
+        check(lib().idf_rans_decode_streams(
+            s, B, ptr(off) + 8 * k0, ptr(word_off) + 8 * k0, ptr(bs.nwords) + 8 * k0, ptr(bs.words),
+            ptr(ws["mean"]), ptr(ws["scale"]), ptr(bs.states) + 8 * k0, ptr(out_state) + 8 * k0,
+            ptr(ws["lat"]), ptr(out_status) + 4 * k0), "rans decode")
+        del k1
+
+
+class ImageCodec:
+    """uint8 NCHW images <-> Bitstream with a FlowEngine (IDFlows configs)."""
+
+    def __init__(self, engine):
+        self.engine = engine
+        self.coder = StreamCoder(engine)
+
+    @torch.no_grad()
+    def encode(self, img_u8: torch.Tensor, cond=None, compact: bool = True) -> Bitstream:
+        _lib.require_device(img_u8, "image batch")
+        if img_u8.dtype != torch.uint8:
+            raise TypeError("ImageCodec.encode expects uint8 images")
+        B = img_u8.shape[0]
+        ws = self.engine.load_u8(img_u8.contiguous())
+        self.engine.forward_pm(B, cond=cond)
+        return self.coder.encode(ws, B, compact=compact)
+
+    @torch.no_grad()
+    def decode(self, bs: Bitstream, cond=None, verify: bool = True):
+        eng = self.engine
+        dev = eng.device
+        B = bs.n_images
+        if bs.states.device != dev:
+            bs = Bitstream(bs.n_images, bs.level_shapes, bs.states.to(dev), bs.nwords.to(dev),
+                           bs.words.to(dev), None, bs.meta)
+        word_off = bs.meta.get("scratch_offsets")
+        if word_off is None:
+            word_off = bs.word_offsets()
+        if bs.words.numel() == 0:
+            bs.words = torch.zeros(1, dtype=torch.int32, device=dev)
+        out_state = torch.empty_like(bs.states)
+        out_status = torch.zeros(bs.n_streams, dtype=torch.int32, device=dev)
+
+        def dec(l, ws):
+            self.coder.decode_level(bs, B, l, ws, word_off, out_state, out_status)
+
+        ws = eng.inverse_pm(B, dec, cond=cond)
+        img, bad = eng.image_u8(ws, B)
+        info = {"final_states": out_state, "status": out_status, "off_grid": bad}
+        if verify:
+            ok = bool((out_state == RANS_L).all().item()) and int(bad.item()) == 0
+            info["ok"] = ok and not bool((out_status & ~_lib.STREAM_WORDS_LEFT).any().item())
+        return img, info

@@ -1,0 +1,52 @@
+"""Model sections of the four north-star configs (BASELINE.json `configs`),
+restated as data from the reference YAML files they cite.  The full YAML files
+(trainers, data loaders, optimisers) are outside this path; a user's own YAML
+loads the same way through load_yaml()."""
+from __future__ import annotations
+
+import copy
+
+import yaml
+
+
+def _dense(growth, depth, act="ReLU"):
+    return {"name": "DenseBlock", "growth_channel": growth, "depth": depth,
+            "layer": {"name": "DenseLayer", "act": act}}
+
+
+def _flows(name, nflows, nsplit, H, W, C, c_nn, p_nn, scale, **extra):
+    d = {"name": name, "nflows": nflows, "nbits": 8, "nsplit": nsplit, "H": H, "W": W, "C": C,
+         "couple": {"name": "AdditiveCouple", "split": 0.75, "nn": c_nn,
+                    "round": {"name": "Round", "nbits": 8}},
+         "extenddim": {"name": "ExtendDim", "scale": scale},
+         "prior": {"name": "Prior", "round": {"name": "Round", "nbits": 8}, "nn": p_nn},
+         "distribution": {"name": "DLogistic"},
+         "round": {"name": "Round", "nbits": 8}}
+    d.update(extra)
+    return d
+
+
+CONFIGS = {
+    # configs/imagenet64.yaml:2-40
+    "imagenet64": _flows("IDFlows", 8, 3, 64, 64, 3, _dense(512, 12), _dense(512, 12), 2),
+    # configs/resflow-cond-imagenet64.yaml:3-44 (flows section)
+    "resflow-cond-imagenet64": _flows("ConditionalFlows", 8, 3, 64, 64, 3, _dense(512, 12),
+                                      _dense(512, 12), 2, conv_for_cond=True),
+    # configs/resflows_smallpatch_split.yaml:3-41 (flows section, 8x8 patches)
+    "resflows_smallpatch_split": _flows("IDFlows", 8, 2, 8, 8, 3, _dense(512, 8), _dense(512, 4), 2),
+    # configs/resflow-patches-vqvae.yaml:3-42 (flows section, 27x23 patches)
+    "resflow-patches-vqvae": _flows("ConditionalFlows", 8, 1, 27, 23, 3,
+                                    _dense(384, 12, "LeakyReLU"), _dense(512, 12, "LeakyReLU"), 1,
+                                    conv_for_cond=False),
+}
+
+
+def get(name: str) -> dict:
+    return copy.deepcopy(CONFIGS[name])
+
+
+def load_yaml(path: str) -> dict:
+    """`train.model` (Trainer) or `train.flows` (ResidualTrainer) of a reference-style YAML."""
+    with open(path) as f:
+        cfg = yaml.safe_load(f)["train"]
+    return cfg.get("model") or cfg.get("flows")

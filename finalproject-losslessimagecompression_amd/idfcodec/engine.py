@@ -1,0 +1,423 @@
+"""FlowEngine: the IDF forward (encode side) and inverse (decode side) on the GPU.
+
+Runs the reference hot path (flows.py:87-152, couplelib.py:47-61,
+priorlib.py:36-47, nnblock.py:53-56, invertible.py:38-48, extenddim.py:23-37)
+entirely through libidfcodec.so kernels.  torch only provides device memory
+and the stream.
+
+HBM layout (per batch of B images):
+  x_l   : two pixel-major buffers per level [B*h_l*w_l, ldx_l] (ping-pong across
+          couplings; the permutation is a gather between them)
+  feat  : DenseBlock feature buffer [P, ld_feat] shared by all blocks
+  tmp   : 1x1-conv output [P, ld_feat]
+  lat / mean / logscale / scale : flat f32 [B * n_sym], level-major, image-minor,
+          NCHW inside -- so rANS stream (image b, level l) is one contiguous run
+          in the reference's symbol order (x[i].reshape(-1), trainer.py:311).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import IdfDenseBlock, IdfHeadOut, check, lib, ptr
+from .packing import PackedBlock, pack_dense_block, round_up
+
+FLOAT = 4
+
+
+class DeviceBlock:
+    """A packed DenseBlock resident in HBM plus its C descriptor."""
+
+    def __init__(self, packed: PackedBlock, device):
+        self.packed = packed
+        self.geom = packed.geom
+        dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
+        self.w1 = [dev(a) for a in packed.w1]
+        self.b1 = [dev(a) for a in packed.b1]
+        self.w3 = [dev(a) for a in packed.w3]
+        self.b3 = [dev(a) for a in packed.b3]
+        self.wh = dev(packed.wh)
+        self.bh = dev(packed.bh)
+        d = IdfDenseBlock()
+        g = self.geom
+        d.depth = g.depth
+        d.act = _lib.ACT[packed.act]
+        d.slope = packed.slope
+        d.g_pad = g.g_pad
+        d.g_alloc = packed.g_alloc
+        for i, k in enumerate(g.k_in):
+            d.k_in[i] = k
+        for i in range(g.depth):
+            d.n1_alloc[i] = packed.n1_alloc[i]
+            d.ldw1[i] = packed.ldw1[i]
+            d.ldw3[i] = packed.ldw3[i]
+            d.w1[i] = self.w1[i].data_ptr()
+            d.b1[i] = self.b1[i].data_ptr()
+            d.w3[i] = self.w3[i].data_ptr()
+            d.b3[i] = self.b3[i].data_ptr()
+        d.n_head = g.n_head
+        d.nh_alloc = packed.nh_alloc
+        d.ldwh = packed.ldwh
+        d.wh = self.wh.data_ptr()
+        d.bh = self.bh.data_ptr()
+        c = g.a
+        for i in range(g.depth):
+            d.c_real[i] = c
+            d.g_real[i] = g.growth[i]
+            c += g.growth[i]
+        d.c_real[g.depth] = c
+        self.desc = d
+        self.timer = None  # an IdfTimer handle: when set, GEMM launches are event-timed
+
+    def run(self, stream, B, H, W, feat, ld_feat, tmp, ld_tmp, head: IdfHeadOut | None):
+        h = ctypes.byref(head) if head else None
+        if self.timer is not None:
+            check(lib().idf_dense_block_f32_timed(stream, ctypes.byref(self.desc), B, H, W, feat,
+                                                  ld_feat, tmp, ld_tmp, h, self.timer),
+                  "idf_dense_block_f32_timed")
+        else:
+            check(lib().idf_dense_block_f32(stream, ctypes.byref(self.desc), B, H, W, feat, ld_feat,
+                                            tmp, ld_tmp, h), "idf_dense_block_f32")
+
+
+def head_couple(mode, out_ptr, ld):
+    h = IdfHeadOut()
+    h.mode = mode
+    h.out = out_ptr
+    h.ld_out = ld
+    h.base = out_ptr
+    h.ld_base = ld
+    return h
+
+
+def head_prior(n_mean, mean_ptr, logscale_ptr, scale_ptr):
+    h = IdfHeadOut()
+    h.mode = _lib.EPI_PRIOR
+    h.n_mean = n_mean
+    h.mean = mean_ptr
+    h.logscale = logscale_ptr
+    h.scale = scale_ptr
+    return h
+
+
+@dataclass
+class Level:
+    C: int          # channels after squeeze
+    h: int
+    w: int
+    a: int          # coupling a_ch (couplelib.py:38)
+    z: int          # latent channels
+    rest: int       # channels passed on (C - z)
+    ldx: int
+    cond_ch: int    # ConditionalFlows cond channels at this level (0 for IDFlows)
+    prior_x_zero: bool  # prior sees zeros for the x part (top level)
+
+    @property
+    def n_sym(self) -> int:
+        return self.z * self.h * self.w
+
+
+class FlowEngine:
+    """Built from a model exposing the reference attributes/state_dict
+    (IDFlows / ConditionalFlows of this package)."""
+
+    def __init__(self, model, device=None):
+        self.device = torch.device(device or "cuda")
+        sd = {k: v for k, v in model.state_dict().items()}
+        self.conditional = type(model).__name__ == "ConditionalFlows"
+        self.conv_for_cond = bool(getattr(model, "conv_for_cond", False))
+        self.nflows = model.nflows
+        self.nsplit = model.nsplit
+        self.C, self.H, self.W = model.C, model.H, model.W
+        self.scale = model.blocks[0]["extend"].scale
+        split = model.blocks[0]["flows"][1].split
+        c_depth = model.blocks[0]["flows"][1].dense.depth
+        c_act = model.blocks[0]["flows"][1].dense.act_name
+        p_depth = model.blocks[0]["prior"].NN.depth
+        p_act = model.blocks[0]["prior"].NN.act_name
+        self.levels: list[Level] = []
+        ch, h, w = self.C, self.H, self.W
+        cond_ch = self.C
+        for l in range(self.nsplit):
+            ch *= self.scale * self.scale
+            h //= self.scale
+            w //= self.scale
+            cond_ch *= self.scale * self.scale
+            top = l == self.nsplit - 1
+            z = ch if top else ch // 2
+            self.levels.append(Level(C=ch, h=h, w=w, a=int(ch * split), z=z, rest=ch - z,
+                                     ldx=round_up(ch, 4),
+                                     cond_ch=cond_ch if self.conditional else 0,
+                                     prior_x_zero=top))
+            if not top:
+                ch -= ch // 2
+        self.n_sym_img = sum(L.n_sym for L in self.levels)
+        # device weights
+        self.couple = []
+        self.prior = []
+        self.ids = []
+        self.inv_ids = []
+        for l in range(self.nsplit):
+            self.couple.append([DeviceBlock(pack_dense_block(
+                sd, f"blocks.{l}.flows.{2 * k + 1}.dense.", c_depth, c_act), self.device)
+                for k in range(self.nflows)])
+            self.prior.append(DeviceBlock(pack_dense_block(sd, f"blocks.{l}.prior.NN.", p_depth,
+                                                           p_act), self.device))
+            ids_l, inv_l = [], []
+            for k in range(self.nflows + 1):
+                Pm = sd[f"blocks.{l}.flows.{2 * k}.P"].detach().float().cpu()
+                ids = torch.argmax(Pm, dim=1).to(torch.int32)
+                inv = torch.empty_like(ids)
+                inv[ids.long()] = torch.arange(ids.numel(), dtype=torch.int32)
+                ids_l.append(ids.to(self.device))
+                inv_l.append(inv.to(self.device))
+            self.ids.append(ids_l)
+            self.inv_ids.append(inv_l)
+        if self.conv_for_cond:
+            self.cond_w = [sd[f"convs.{l}.weight"].detach().float().contiguous().to(self.device)
+                           for l in range(self.nsplit)]
+            self.cond_b = [sd[f"convs.{l}.bias"].detach().float().contiguous().to(self.device)
+                           for l in range(self.nsplit)]
+        blocks = [b for lv in self.couple for b in lv] + self.prior
+        self.ld_feat = max(b.geom.ld_feat for b in blocks)
+        self._ws = {}
+        self._top_prior = None
+
+    # ------------------------------------------------------------ geometry
+    def sym_offsets(self, B: int) -> list[int]:
+        """start of each level's block in the flat latent buffers"""
+        offs, o = [], 0
+        for L in self.levels:
+            offs.append(o)
+            o += B * L.n_sym
+        offs.append(o)
+        return offs
+
+    def flops_per_image(self) -> dict:
+        """algorithmic FLOPs of one image per direction (unpadded, as the reference)"""
+        c = p = 0
+        for l, L in enumerate(self.levels):
+            hw = L.h * L.w
+            c += hw * sum(b.geom.flops_per_pixel() for b in self.couple[l])
+            p += hw * self.prior[l].geom.flops_per_pixel()
+        return {"couple": c, "prior": p, "total": c + p}
+
+    # ------------------------------------------------------------ workspace
+    def workspace(self, B: int):
+        ws = self._ws.get(B)
+        if ws is not None:
+            return ws
+        dev = self.device
+        f = lambda n: torch.empty(int(n), dtype=torch.float32, device=dev)  # noqa: E731
+        Pmax = max(B * L.h * L.w for L in self.levels)
+        ws = {
+            "img": f(B * self.H * self.W * 4),
+            "x": [[f(B * L.h * L.w * L.ldx), f(B * L.h * L.w * L.ldx)] for L in self.levels],
+            "feat": f(Pmax * self.ld_feat),
+            "tmp": f(Pmax * self.ld_feat),
+            "lat": f(B * self.n_sym_img),
+            "mean": f(B * self.n_sym_img),
+            "logscale": f(B * self.n_sym_img),
+            "scale": f(B * self.n_sym_img),
+            "cur": [0] * self.nsplit,
+        }
+        if self.conditional:
+            ws["cond"] = [f(B * L.h * L.w * round_up(L.cond_ch, 4)) for L in self.levels]
+            ws["cond_img"] = f(B * self.H * self.W * 4)
+        self._ws = {B: ws}  # keep one batch size resident
+        return ws
+
+    # ------------------------------------------------------------ pieces
+    def _x(self, ws, l, which=0):
+        return ws["x"][l][(ws["cur"][l] + which) % 2]
+
+    def _swap(self, ws, l):
+        ws["cur"][l] ^= 1
+
+    def _prep_cond(self, ws, B, cond_nchw, s):
+        """ConditionalFlows cond at each level: ExtendDim of the cond image
+        (flows.py:309) or the stride-2 convs (flows.py:310-313)."""
+        L = lib()
+        check(L.idf_nchw_to_pm(s, B, self.C, self.H, self.W, ptr(cond_nchw), ptr(ws["cond_img"]), 4),
+              "nchw_to_pm")
+        src, ld, H, W, C = ws["cond_img"], 4, self.H, self.W, self.C
+        for l, Lv in enumerate(self.levels):
+            dst, ldd = ws["cond"][l], round_up(Lv.cond_ch, 4)
+            if self.conv_for_cond:
+                check(L.idf_conv4x4s2_f32(s, B, H, W, C, Lv.cond_ch, ptr(src), ld,
+                                          ptr(self.cond_w[l]), ptr(self.cond_b[l]), ptr(dst), ldd),
+                      "conv4x4s2")
+            else:
+                check(L.idf_squeeze(s, B, H, W, C, self.scale, ptr(src), ld, ptr(dst), ldd),
+                      "squeeze")
+            src, ld, H, W, C = dst, ldd, Lv.h, Lv.w, Lv.cond_ch
+
+    def _prior(self, ws, B, l, s, mean, logscale, scale, x_src=None, ld_src=0):
+        """Prior.forward (priorlib.py:36-47) on pixel-major input written into feat."""
+        L = lib()
+        Lv = self.levels[l]
+        blk = self.prior[l]
+        P = B * Lv.h * Lv.w
+        feat = ws["feat"]
+        ld = self.ld_feat
+        nx = Lv.C if Lv.prior_x_zero else Lv.rest
+        a_pad = blk.geom.a_pad
+        if self.conditional:
+            if Lv.prior_x_zero:
+                check(L.idf_copy_cols(s, P, 0, nx, None, 0, ptr(feat), ld), "zero cols")
+            else:
+                check(L.idf_copy_cols(s, P, nx, nx, x_src, ld_src, ptr(feat), ld), "copy cols")
+            check(L.idf_copy_cols(s, P, Lv.cond_ch, a_pad - nx, ptr(ws["cond"][l]),
+                                  round_up(Lv.cond_ch, 4), ptr(feat) + nx * FLOAT, ld), "cond cols")
+        elif Lv.prior_x_zero:
+            check(L.idf_copy_cols(s, P, 0, a_pad, None, 0, ptr(feat), ld), "zero cols")
+        else:
+            check(L.idf_copy_cols(s, P, nx, a_pad, x_src, ld_src, ptr(feat), ld), "copy cols")
+        blk.run(s, B, Lv.h, Lv.w, ptr(feat), ld, ptr(ws["tmp"]), ld,
+                head_prior(Lv.z, mean, logscale, scale))
+
+    def _top_prior_cached(self, ws, B, s, off):
+        """IDFlows' top prior sees zeros (priorlib.py:43): its output does not depend on
+        the data, so it is computed once (batch 1) and replicated per image."""
+        Lv = self.levels[-1]
+        n = Lv.n_sym
+        if self._top_prior is None:
+            tp = torch.empty(3 * n, dtype=torch.float32, device=self.device)
+            ws1 = {"feat": ws["feat"], "tmp": ws["tmp"]}
+            self._prior(ws1, 1, self.nsplit - 1, s, ptr(tp), ptr(tp) + n * FLOAT,
+                        ptr(tp) + 2 * n * FLOAT)
+            self._top_prior = tp.view(3, n)
+        for i, key in enumerate(("mean", "logscale", "scale")):
+            ws[key][off: off + B * n].view(B, n).copy_(self._top_prior[i].expand(B, n))
+
+    # ------------------------------------------------------------ forward
+    @torch.no_grad()
+    def forward_pm(self, B: int, cond=None):
+        """Runs flows.py:87-116 from ws['img'] (pixel-major, ld 4) for B images.
+        Fills ws lat/mean/logscale/scale.  Returns the workspace."""
+        L = lib()
+        ws = self.workspace(B)
+        s = _lib.stream_ptr(self.device)
+        offs = self.sym_offsets(B)
+        if self.conditional:
+            self._prep_cond(ws, B, cond, s)
+        src, ld_src, H, W, C = ptr(ws["img"]), 4, self.H, self.W, self.C
+        for l, Lv in enumerate(self.levels):
+            ws["cur"][l] = 0
+            P = B * Lv.h * Lv.w
+            check(L.idf_squeeze(s, B, H, W, C, self.scale, src, ld_src, ptr(self._x(ws, l)), Lv.ldx),
+                  "squeeze")
+            for k in range(self.nflows):
+                blk = self.couple[l][k]
+                x, x2 = self._x(ws, l), self._x(ws, l, 1)
+                check(L.idf_permute_couple_in(s, P, Lv.C, ptr(self.ids[l][k]), ptr(x), Lv.ldx, ptr(x2),
+                                              Lv.ldx, Lv.a, blk.geom.a_pad, ptr(ws["feat"]),
+                                              self.ld_feat), "permute")
+                self._swap(ws, l)
+                xo = ptr(x2) + Lv.a * FLOAT
+                blk.run(s, B, Lv.h, Lv.w, ptr(ws["feat"]), self.ld_feat, ptr(ws["tmp"]), self.ld_feat,
+                        head_couple(_lib.EPI_COUPLE_ADD, xo, Lv.ldx))
+            x, x2 = self._x(ws, l), self._x(ws, l, 1)
+            check(L.idf_permute_couple_in(s, P, Lv.C, ptr(self.ids[l][self.nflows]), ptr(x), Lv.ldx,
+                                          ptr(x2), Lv.ldx, 0, 0, None, 0), "permute")
+            self._swap(ws, l)
+            x = self._x(ws, l)
+            o = offs[l]
+            check(L.idf_pm_to_nchw(s, B, Lv.z, Lv.h, Lv.w, ptr(x), Lv.ldx,
+                                   ptr(ws["lat"]) + o * FLOAT), "pm_to_nchw")
+            mean, logs, scale = (ptr(ws[k]) + o * FLOAT for k in ("mean", "logscale", "scale"))
+            if Lv.prior_x_zero and not self.conditional:
+                self._top_prior_cached(ws, B, s, o)
+            else:
+                self._prior(ws, B, l, s, mean, logs, scale, ptr(x) + Lv.z * FLOAT, Lv.ldx)
+            src, ld_src, H, W, C = ptr(x) + Lv.z * FLOAT, Lv.ldx, Lv.h, Lv.w, Lv.rest
+        return ws
+
+    def load_u8(self, img_u8: torch.Tensor):
+        B = img_u8.shape[0]
+        ws = self.workspace(B)
+        check(lib().idf_dequant_u8(_lib.stream_ptr(self.device), B, self.C, self.H, self.W,
+                                   ptr(img_u8), ptr(ws["img"]), 4), "dequant")
+        return ws
+
+    def load_nchw(self, x: torch.Tensor):
+        B = x.shape[0]
+        ws = self.workspace(B)
+        x = x.contiguous().float()
+        check(lib().idf_nchw_to_pm(_lib.stream_ptr(self.device), B, self.C, self.H, self.W, ptr(x),
+                                   ptr(ws["img"]), 4), "nchw_to_pm")
+        return ws
+
+    # ------------------------------------------------------------ inverse
+    @torch.no_grad()
+    def inverse_pm(self, B: int, decode_level, cond=None, priors: bool = True):
+        """Top-down decoder (flows.py:118-152 order).  For each level l (top first):
+        prior -> decode_level(l, ws) fills ws['lat'] level l -> flows backward ->
+        unsqueeze.  The image lands in ws['img'] (pixel-major, ld 4)."""
+        L = lib()
+        ws = self.workspace(B)
+        s = _lib.stream_ptr(self.device)
+        offs = self.sym_offsets(B)
+        if self.conditional and priors:
+            self._prep_cond(ws, B, cond, s)
+        for l in reversed(range(self.nsplit)):
+            Lv = self.levels[l]
+            P = B * Lv.h * Lv.w
+            x = self._x(ws, l)
+            o = offs[l]
+            if priors:
+                mean, logs, scale = (ptr(ws[k]) + o * FLOAT for k in ("mean", "logscale", "scale"))
+                if Lv.prior_x_zero and not self.conditional:
+                    self._top_prior_cached(ws, B, s, o)
+                else:
+                    self._prior(ws, B, l, s, mean, logs, scale, ptr(x) + Lv.z * FLOAT, Lv.ldx)
+            decode_level(l, ws)
+            check(L.idf_nchw_to_pm(s, B, Lv.z, Lv.h, Lv.w, ptr(ws["lat"]) + o * FLOAT, ptr(x),
+                                   Lv.ldx), "nchw_to_pm")
+            x2 = self._x(ws, l, 1)
+            check(L.idf_permute_couple_in(s, P, Lv.C, ptr(self.inv_ids[l][self.nflows]), ptr(x),
+                                          Lv.ldx, ptr(x2), Lv.ldx, 0, 0, None, 0), "permute")
+            self._swap(ws, l)
+            for k in reversed(range(self.nflows)):
+                blk = self.couple[l][k]
+                x, x2 = self._x(ws, l), self._x(ws, l, 1)
+                check(L.idf_copy_cols(s, P, Lv.a, blk.geom.a_pad, ptr(x), Lv.ldx, ptr(ws["feat"]),
+                                      self.ld_feat), "copy cols")
+                xo = ptr(x) + Lv.a * FLOAT
+                blk.run(s, B, Lv.h, Lv.w, ptr(ws["feat"]), self.ld_feat, ptr(ws["tmp"]), self.ld_feat,
+                        head_couple(_lib.EPI_COUPLE_SUB, xo, Lv.ldx))
+                check(L.idf_permute_couple_in(s, P, Lv.C, ptr(self.inv_ids[l][k]), ptr(x), Lv.ldx,
+                                              ptr(x2), Lv.ldx, 0, 0, None, 0), "permute")
+                self._swap(ws, l)
+            x = self._x(ws, l)
+            if l > 0:
+                Lp = self.levels[l - 1]
+                dst, ldd = ptr(self._x(ws, l - 1)) + Lp.z * FLOAT, Lp.ldx
+                Hh, Ww, Cc = Lp.h, Lp.w, Lp.rest
+            else:
+                dst, ldd, Hh, Ww, Cc = ptr(ws["img"]), 4, self.H, self.W, self.C
+            check(L.idf_unsqueeze(s, B, Hh, Ww, Cc, self.scale, ptr(x), Lv.ldx, dst, ldd),
+                  "unsqueeze")
+        return ws
+
+    def image_nchw(self, ws, B):
+        out = torch.empty((B, self.C, self.H, self.W), dtype=torch.float32, device=self.device)
+        check(lib().idf_pm_to_nchw(_lib.stream_ptr(self.device), B, self.C, self.H, self.W,
+                                   ptr(ws["img"]), 4, ptr(out)), "pm_to_nchw")
+        return out
+
+    def image_u8(self, ws, B):
+        out = torch.empty((B, self.C, self.H, self.W), dtype=torch.uint8, device=self.device)
+        bad = torch.zeros(1, dtype=torch.int32, device=self.device)
+        check(lib().idf_quant_u8(_lib.stream_ptr(self.device), B, self.C, self.H, self.W,
+                                 ptr(ws["img"]), 4, ptr(out), ptr(bad)), "quant")
+        return out, bad
+
+    def level_views(self, ws, B, key):
+        offs = self.sym_offsets(B)
+        return [ws[key][offs[l]: offs[l + 1]].view(B, L.z, L.h, L.w)
+                for l, L in enumerate(self.levels)]

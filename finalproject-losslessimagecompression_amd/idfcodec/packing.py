@@ -1,0 +1,167 @@
+"""Host-side weight packing of a DenseBlock (nnblock.py:24-56) for the HIP kernels.
+
+The feature buffer of a DenseBlock is pixel-major with *padded* channel
+segments: the block input (a channels) occupies columns [0, a_pad), layer i's
+growth (g_i channels, g_i = (i+1)G//d - iG//d, nnblock.py:44) occupies
+[a_pad + i*g_pad, a_pad + i*g_pad + g_i), and the padding columns are always
+zero.  k_in[i] = a_pad + i*g_pad is the padded width layer i reads.  Weights are
+scattered into that padded coordinate system with zeros elsewhere, so every
+GEMM has K a multiple of 4, unmasked weight tiles, and padded outputs of 0.
+
+Pure numpy: runs (and is tested) without a GPU.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+
+def round_up(v: int, m: int) -> int:
+    return ((v + m - 1) // m) * m
+
+
+def tile_n(n: int) -> int:
+    """Output-column tile of the GEMM kernels (must match flow_kernels.hip tile_n)."""
+    if n <= 16:
+        return 16
+    if n <= 32:
+        return 32
+    if n <= 48:
+        return 48
+    if n <= 64:
+        return 64
+    w64 = round_up(n, 64) - n
+    w128 = round_up(n, 128) - n
+    return 128 if w128 <= w64 + 32 else 64
+
+
+def growths(growth_channel: int, depth: int) -> list[int]:
+    """nnblock.py:43-46."""
+    return [(i + 1) * growth_channel // depth - i * growth_channel // depth for i in range(depth)]
+
+
+@dataclass
+class BlockGeometry:
+    a: int                 # block input channels
+    depth: int
+    growth: list[int]
+    n_head: int
+    a_pad: int = 0
+    g_pad: int = 0
+    k_in: list[int] = field(default_factory=list)
+
+    def __post_init__(self):
+        self.a_pad = round_up(self.a, 4)
+        self.g_pad = round_up(max(self.growth) if self.growth else 4, 4)
+        self.k_in = [self.a_pad + i * self.g_pad for i in range(self.depth + 1)]
+
+    @property
+    def width(self) -> int:
+        """padded channels of the full feature buffer"""
+        return self.k_in[self.depth]
+
+    @property
+    def ld_feat(self) -> int:
+        return round_up(self.width, 16)
+
+    def pos(self, ch: int) -> int:
+        """padded column of logical channel `ch` of the concatenated features"""
+        if ch < self.a:
+            return ch
+        r = ch - self.a
+        for j, g in enumerate(self.growth):
+            if r < g:
+                return self.a_pad + j * self.g_pad + r
+            r -= g
+        raise IndexError(ch)
+
+    def positions(self, n: int) -> np.ndarray:
+        return np.array([self.pos(c) for c in range(n)], dtype=np.int64)
+
+    def flops_per_pixel(self) -> int:
+        """algorithmic FLOPs of the block per pixel (unpadded, as the reference)"""
+        f = 0
+        c = self.a
+        for g in self.growth:
+            f += 2 * c * c + 2 * 9 * c * g
+            c += g
+        return f + 2 * c * self.n_head
+
+
+@dataclass
+class PackedBlock:
+    geom: BlockGeometry
+    act: str
+    slope: float
+    w1: list[np.ndarray]
+    b1: list[np.ndarray]
+    w3: list[np.ndarray]
+    b3: list[np.ndarray]
+    wh: np.ndarray
+    bh: np.ndarray
+    g_alloc: int
+    n1_alloc: list[int]
+    ldw1: list[int]
+    ldw3: list[int]
+    nh_alloc: int
+    ldwh: int
+
+
+def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
+                     slope: float = 0.01) -> PackedBlock:
+    """Pack the reference DenseBlock parameters found under `prefix` in `sd`
+    (keys `{prefix}layers.{i}.layers.{0,1}.{weight,bias}`, head `{prefix}layers.{depth}.*`)."""
+    def arr(k):
+        v = sd[prefix + k]
+        if hasattr(v, "detach"):
+            v = v.detach().cpu().numpy()
+        return np.asarray(v, dtype=np.float32)
+
+    w10 = arr("layers.0.layers.0.weight")
+    a = int(w10.shape[1])
+    gs = [int(arr(f"layers.{i}.layers.1.weight").shape[0]) for i in range(depth)]
+    wh_src = arr(f"layers.{depth}.weight")
+    n_head = int(wh_src.shape[0])
+    geom = BlockGeometry(a=a, depth=depth, growth=gs, n_head=n_head)
+    g_alloc = round_up(geom.g_pad, tile_n(geom.g_pad))
+    w1s, b1s, w3s, b3s, n1s, ld1s, ld3s = [], [], [], [], [], [], []
+    c = a
+    for i in range(depth):
+        k = geom.k_in[i]
+        pos = geom.positions(c)
+        w1 = arr(f"layers.{i}.layers.0.weight")[:, :, 0, 0]  # [c, c]
+        b1 = arr(f"layers.{i}.layers.0.bias")
+        w3 = arr(f"layers.{i}.layers.1.weight")             # [g, c, 3, 3]
+        b3 = arr(f"layers.{i}.layers.1.bias")
+        assert w1.shape == (c, c) and w3.shape[1] == c, (w1.shape, w3.shape, c)
+        n1_alloc = round_up(k, tile_n(k))
+        ldw1 = round_up(k, 16)
+        w1p = np.zeros((n1_alloc, ldw1), np.float32)
+        w1p[np.ix_(pos, pos)] = w1
+        b1p = np.zeros(n1_alloc, np.float32)
+        b1p[pos] = b1
+        ldw3 = round_up(k, 16)
+        w3p = np.zeros((g_alloc, 9, ldw3), np.float32)
+        g = w3.shape[0]
+        # [g, c, ky, kx] -> [g, tap=ky*3+kx, pos(c)]
+        w3p[:g][:, :, pos] = w3.reshape(g, c, 9).transpose(0, 2, 1)
+        b3p = np.zeros(g_alloc, np.float32)
+        b3p[:g] = b3
+        w1s.append(w1p); b1s.append(b1p); w3s.append(w3p); b3s.append(b3p)
+        n1s.append(n1_alloc); ld1s.append(ldw1); ld3s.append(ldw3)
+        c += g
+    kh = geom.k_in[depth]
+    ldwh = round_up(kh, 16)
+    nh_alloc = round_up(n_head, tile_n(n_head))
+    whp = np.zeros((nh_alloc, ldwh), np.float32)
+    whp[:n_head][:, geom.positions(c)] = wh_src[:, :, 0, 0]
+    bhp = np.zeros(nh_alloc, np.float32)
+    bhp[:n_head] = arr(f"layers.{depth}.bias")
+    return PackedBlock(geom, act, slope, w1s, b1s, w3s, b3s, whp, bhp, g_alloc, n1s, ld1s, ld3s,
+                       nh_alloc, ldwh)
+
+
+def unpack_features(feat: np.ndarray, geom: BlockGeometry, n: int) -> np.ndarray:
+    """Logical [P, n] view of the first n concatenated channels of a padded feature buffer."""
+    return feat[:, geom.positions(n)]

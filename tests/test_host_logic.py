@@ -1,0 +1,243 @@
+"""Host-side logic on CPU: C-ABI exports, weight packing, mirror modules,
+bitstream container, coder chaining, expf restatement (exhaustive)."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+import yaml
+
+from conftest import PKG, REPO
+
+
+# ------------------------------------------------------------------ C ABI
+def _header_functions():
+    src = open(os.path.join(REPO, "include", "idf_codec.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[A-Za-z_0-9]+\s*\*?\s*(idf_[a-z0-9_]+)\s*\(", src,
+                                 flags=re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    import ctypes
+    from idfcodec import _lib
+    names = _header_functions()
+    assert len(names) >= 20
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    for n in names:
+        assert hasattr(L, n), f"{n} declared in include/idf_codec.h but not exported"
+    assert set(names) == set(_lib.SIGNATURES), "ctypes signatures out of sync with the header"
+    lib = _lib.lib()
+    assert lib.idf_version().decode().startswith("idfcodec")
+
+
+def test_struct_layout_matches_header():
+    """ctypes mirror of IdfDenseBlock / IdfHeadOut == the C layout (compiled probe)."""
+    from idfcodec import _lib
+    import ctypes
+    probe = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "idf_codec.h"
+int main(){printf("%zu %zu %zu %zu %zu %zu\n", sizeof(IdfDenseBlock), offsetof(IdfDenseBlock,w1),
+ offsetof(IdfDenseBlock,n_head), offsetof(IdfDenseBlock,bh), sizeof(IdfHeadOut), offsetof(IdfHeadOut,scale));}
+'''
+    import tempfile
+    with tempfile.TemporaryDirectory() as t:
+        c = os.path.join(t, "p.c")
+        open(c, "w").write(probe)
+        exe = os.path.join(t, "p")
+        subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), c, "-o", exe], check=True)
+        got = list(map(int, subprocess.run([exe], capture_output=True, text=True).stdout.split()))
+    D, H = _lib.IdfDenseBlock, _lib.IdfHeadOut
+    assert got == [ctypes.sizeof(D), D.w1.offset, D.n_head.offset, D.bh.offset, ctypes.sizeof(H),
+                   H.scale.offset]
+
+
+# ------------------------------------------------------------------ packing
+def _simulate_packed_block(pb, x):
+    """The device algorithm (padded pixel-major GEMMs) replayed with torch on CPU."""
+    from idfcodec.packing import round_up
+    g = pb.geom
+    B, C, H, W = x.shape
+    P = B * H * W
+    feat = torch.zeros(P, g.ld_feat, dtype=torch.float64)
+    feat[:, :C] = x.permute(0, 2, 3, 1).reshape(P, C).double()
+    act = {"ReLU": F.relu, "LeakyReLU": lambda v: F.leaky_relu(v, 0.01)}[pb.act]
+    for i in range(g.depth):
+        k = g.k_in[i]
+        w1 = torch.from_numpy(pb.w1[i]).double()
+        T = feat[:, :k] @ w1[:k, :k].T + torch.from_numpy(pb.b1[i]).double()[:k]
+        Tn = T.view(B, H, W, k).permute(0, 3, 1, 2)
+        w3 = torch.from_numpy(pb.w3[i]).double()[: g.g_pad, :, :k]  # [g, tap, c]
+        w3c = w3.permute(0, 2, 1).reshape(g.g_pad, k, 3, 3)
+        o = F.conv2d(Tn, w3c, torch.from_numpy(pb.b3[i]).double()[: g.g_pad], padding=1)
+        feat[:, k:k + g.g_pad] = act(o).permute(0, 2, 3, 1).reshape(P, g.g_pad)
+    kh = g.k_in[g.depth]
+    out = feat[:, :kh] @ torch.from_numpy(pb.wh).double()[: g.n_head, :kh].T + \
+        torch.from_numpy(pb.bh).double()[: g.n_head]
+    del round_up
+    return out.view(B, H, W, g.n_head).permute(0, 3, 1, 2)
+
+
+@pytest.mark.parametrize("name", ["t1_idflows_2lvl", "t2_idflows_3lvl_leaky", "t4_cond_s1_odd"])
+def test_packed_layout_reproduces_dense_block(golden, name):
+    import flow_oracle as FO
+    from idfcodec.packing import pack_dense_block
+    d = golden(f"flow_{name}.npz")
+    cfg = yaml.safe_load(bytes(d["cfg_yaml"]).decode())
+    sd = {k[3:]: torch.from_numpy(d[k]) for k in d.files if k.startswith("sd/")}
+    depth = cfg["couple"]["nn"]["depth"]
+    act = cfg["couple"]["nn"]["layer"]["act"]
+    prefix = "blocks.0.flows.1.dense."
+    pb = pack_dense_block(sd, prefix, depth, act)
+    a = pb.geom.a
+    x = torch.randn(2, a, cfg["H"] // cfg["extenddim"]["scale"], cfg["W"] // cfg["extenddim"]["scale"],
+                    generator=torch.Generator().manual_seed(5))
+    ref = FO.dense_block(x.double(), {k: v.double() for k, v in sd.items()}, prefix, depth, act)
+    got = _simulate_packed_block(pb, x)
+    torch.testing.assert_close(got, ref, rtol=1e-9, atol=1e-9)
+    # padding columns are exactly zero in every weight
+    g = pb.geom
+    pad_cols = sorted(set(range(g.width)) - set(g.positions(g.a + sum(g.growth)).tolist()))
+    assert np.all(pb.wh[:, pad_cols] == 0)
+
+
+def test_tile_n_matches_kernel_source():
+    from idfcodec.packing import tile_n
+    src = open(os.path.join(PKG, "csrc", "flow_kernels.hip")).read()
+    assert "static int tile_n(int N)" in src
+    assert [tile_n(n) for n in (3, 16, 17, 44, 48, 64, 65, 96, 128, 200, 540)] == \
+        [16, 16, 32, 48, 48, 64, 128, 128, 128, 128, 64]
+
+
+def test_flops_per_image_imagenet64():
+    """51.41 GFLOP per image per direction (measured with hooks)."""
+    from idfcodec.packing import BlockGeometry, growths
+    tot = 0
+    for C, hw in ((12, 32 * 32), (24, 16 * 16), (48, 8 * 8)):
+        a = int(C * 0.75)
+        cg = BlockGeometry(a=a, depth=12, growth=growths(512, 12), n_head=C - a)
+        tot += 8 * hw * cg.flops_per_pixel()
+    for cin, out, hw in ((6, 12, 32 * 32), (12, 24, 16 * 16), (48, 96, 8 * 8)):
+        pg = BlockGeometry(a=cin, depth=12, growth=growths(512, 12), n_head=out)
+        tot += hw * pg.flops_per_pixel()
+    assert abs(tot / 1e9 - 51.41) < 0.05, tot
+
+
+# ------------------------------------------------------------------ mirror modules
+@pytest.mark.parametrize("name", ["t1_idflows_2lvl", "t2_idflows_3lvl_leaky", "t3_cond_convcond",
+                                  "t4_cond_s1_odd"])
+def test_seeded_mirror_model_equals_reference(golden, name):
+    from idfcodec import synthetic
+    d = golden(f"flow_{name}.npz")
+    cfg = yaml.safe_load(bytes(d["cfg_yaml"]).decode())
+    sd = synthetic.build_model(cfg).state_dict()
+    ref = {k[3:]: d[k] for k in d.files if k.startswith("sd/")}
+    assert list(sd) == list(ref)
+    for k in ref:
+        assert np.array_equal(sd[k].numpy(), ref[k]), k
+
+
+@pytest.mark.slow
+def test_seeded_imagenet64_equals_reference(golden):
+    from idfcodec import configs, synthetic
+    d = golden("imagenet64_b2.npz")
+    sd = synthetic.build_model(configs.get("imagenet64")).state_dict()
+    assert list(sd) == bytes(d["param_names"]).decode().split("\n")
+    sums = np.array([float(v.double().sum()) for v in sd.values()])
+    assert np.array_equal(sums, d["param_sums"])
+
+
+def test_configs_restate_reference_yaml():
+    from idfcodec import configs
+    ref_dir = "/root/reference/configs"
+    if not os.path.isdir(ref_dir):
+        pytest.skip("reference tree not present (GPU box)")
+    for n in configs.CONFIGS:
+        assert configs.load_yaml(os.path.join(ref_dir, n + ".yaml")) == configs.get(n)
+
+
+def test_registry_names():
+    import flows  # noqa: F401
+    from moduleregister import Register
+    for n in ("IDFlows", "ConditionalFlows", "AdditiveCouple", "DenseBlock", "DenseLayer", "Prior",
+              "ExtendDim", "DLogistic", "Round"):
+        assert Register.get(n).__name__ == n
+    with pytest.raises(Exception, match="Can not find object"):
+        Register.get("NoSuchThing")
+
+
+def test_product_modules_refuse_cpu_tensors():
+    from idfcodec import configs, synthetic
+    from idfcodec._lib import IdfError
+    m = synthetic.build_model(configs.get("imagenet64"))
+    with pytest.raises((IdfError, RuntimeError)):
+        m.forward(torch.zeros(1, 3, 64, 64), None)
+    with pytest.raises((IdfError, RuntimeError)):
+        m.blocks[0]["flows"][1].dense(torch.zeros(1, 9, 4, 4))
+
+
+# ------------------------------------------------------------------ bitstream
+def test_bitstream_container_roundtrip():
+    from idfcodec.codec import Bitstream
+    g = torch.Generator().manual_seed(0)
+    nw = torch.randint(0, 50, (6,), generator=g).to(torch.int64)
+    st = torch.randint(-(2 ** 62), 2 ** 62, (6,), generator=g, dtype=torch.int64)
+    w = torch.randint(-(2 ** 31), 2 ** 31 - 1, (int(nw.sum()),), generator=g, dtype=torch.int32)
+    bs = Bitstream(2, [(6, 32, 32), (12, 16, 16), (48, 8, 8)], st, nw, w,
+                   meta={"n_subpixels": 2 * 3 * 64 * 64})
+    raw = bs.to_bytes()
+    bs2 = Bitstream.from_bytes(raw)
+    assert bs2.n_images == 2 and bs2.level_shapes == bs.level_shapes
+    assert torch.equal(bs2.states, st) and torch.equal(bs2.nwords, nw) and torch.equal(bs2.words, w)
+    assert bs2.bits() == 64 * 6 + 32 * int(nw.sum())
+    assert len(raw) == 20 + 36 + 8 + 8 * 6 + 4 * 6 + 4 * int(nw.sum())
+    with pytest.raises(ValueError):
+        Bitstream.from_bytes(b"XXXX" + raw[4:])
+
+
+# ------------------------------------------------------------------ coder chaining (F4)
+def test_coder_decode_fix_roundtrips_with_oracle(golden, oracle, monkeypatch):
+    """coder.Encode chains the state across levels; the reference Decode does not
+    round-trip, the fixed Decode does.  Exercised on CPU with the
+    oracle standing in for rans.rans (same list API)."""
+    import coder
+
+    def enc(state, n, x, m, s):
+        st, w = oracle.encode(state, x[:n], m[:n], s[:n])
+        return st, w.tolist()
+
+    def dec(state, buf, n, m, s):
+        # reference convention: buf, m, s reversed; result reversed
+        st, out = oracle.decode(state, np.asarray(buf[::-1], np.uint32), n, np.asarray(m[::-1]),
+                                np.asarray(s[::-1]))
+        return st, out[::-1].astype(np.float64).tolist()
+
+    monkeypatch.setattr(coder, "encode", enc)
+    monkeypatch.setattr(coder, "decode", dec)
+    d = golden("imagenet64_b2.npz")
+    lat = [torch.from_numpy(d[f"latent{i}"]) for i in range(3)]
+    mean = [torch.from_numpy(d[f"mean{i}"]) for i in range(3)]
+    logs = [torch.from_numpy(d[f"logscale{i}"]) for i in range(3)]
+    x, bufs = coder.Encode(lat, mean, logs)
+    assert any(len(b) for b in bufs)
+    x2, rec = coder.Decode(bufs, mean, logs, x)
+    assert x2 == 1 << 32
+    for a, b in zip(rec, lat):
+        assert torch.equal(a, b)
+
+
+# ------------------------------------------------------------------ expf restatement
+@pytest.mark.slow
+def test_restated_expf_equals_libm_on_all_floats(tmp_path):
+    exe = tmp_path / "expf_check"
+    subprocess.run(["g++", "-O2", "-ffp-contract=off", "-fopenmp", "-I", os.path.join(PKG, "csrc"),
+                    os.path.join(REPO, "tests", "native", "expf_check.cpp"), "-o", str(exe)],
+                   check=True, capture_output=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout
+    assert "mismatches=0" in r.stdout
