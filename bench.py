@@ -218,6 +218,9 @@ def main():
             "bits_per_subpixel": round(bpp / 3, 4),
             "round_trip_exact": exact,
             "flow_tflops_per_direction": round(B * flops / 1e12, 4),
+            "flow_tflops_executed_per_direction": round(
+                B * eng.flops_per_image(fold=eng.fold)["total"] / 1e12, 4),
+            "fold_1x1_into_3x3": eng.fold,
             "roofline": {
                 "kernel": "gemm_f32_kernel<256,48,4,1,MODE_CONV3,EPI_ACT> (3x3 conv, implicit GEMM)",
                 "bound": "mfma",

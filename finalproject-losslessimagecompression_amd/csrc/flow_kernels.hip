@@ -37,7 +37,14 @@ namespace idf {
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 enum { MODE_DENSE = 0, MODE_CONV3 = 1 };
-enum { EPI_STORE = 0, EPI_ACT = 1, EPI_COUPLE_ADD = 2, EPI_COUPLE_SUB = 3, EPI_PRIOR = 4 };
+// EPI_ACT_FOLD: the 3x3 conv of a DenseLayer with its 1x1 conv folded in
+// (W' = W3[tap] . W1 applied to the layer input directly).  The 1x1 bias b1 then
+// enters as v[tap] = W3[tap] . b1 for every tap whose neighbour lies inside the
+// image (the reference zero-pads the 1x1 OUTPUT, nnlayer.py:43-45), so the bias
+// of pixel (y, x) is b3 + sum of v over its valid taps; `bfull` holds that sum for
+// interior pixels, computed in the same fp32 order as the border loop.
+enum { EPI_STORE = 0, EPI_ACT = 1, EPI_COUPLE_ADD = 2, EPI_COUPLE_SUB = 3, EPI_PRIOR = 4,
+       EPI_ACT_FOLD = 5 };
 
 struct GemmArgs {
   int64_t P;        // rows (pixels)
@@ -59,6 +66,9 @@ struct GemmArgs {
   int32_t B, H, Wd;   // image geometry (CONV3 neighbours, PRIOR NCHW)
   int32_t act;
   float slope;
+  const float* vtap;  // ACT_FOLD: [9][ldv] per-tap folded 1x1 bias
+  const float* bfull; // ACT_FOLD: interior bias b3 + sum_tap vtap
+  int32_t ldv;
   int32_t m_tiles, n_tiles;
 };
 
@@ -84,7 +94,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE, int EPI>
 __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmArgs g) {
   constexpr int BK = 16;
-  constexpr int LDS_LD = BK + 4;
+  constexpr int LDS_LD = BK + 8;  // 96-B rows: b128 fragment reads are bank-conflict free
   constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
   constexpr int FM = WTM / 16, FN = WTN / 16;
   constexpr int A_F4 = BM * 4;                    // float4s per A chunk
@@ -230,6 +240,21 @@ __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmArgs g) {
           g.out[p * g.ldo + n] = v;
         } else if (EPI == EPI_ACT) {
           g.out[p * g.ldo + n] = apply_act(v, g.act, g.slope);
+        } else if (EPI == EPI_ACT_FOLD) {
+          const int64_t rem = p % hw;
+          const int y = (int)(rem / g.Wd), x = (int)(rem % g.Wd);
+          float bsum;
+          if (y >= 1 && y <= g.H - 2 && x >= 1 && x <= g.Wd - 2) {
+            bsum = g.bfull[n];
+          } else {
+            bsum = bv;  // b3, then + v[tap] for every in-image tap, fixed order
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+              const int ny = y + tap / 3 - 1, nx = x + tap % 3 - 1;
+              if (ny >= 0 && ny < g.H && nx >= 0 && nx < g.Wd) bsum = bsum + g.vtap[tap * g.ldv + n];
+            }
+          }
+          g.out[p * g.ldo + n] = apply_act(acc[i][j][r] + bsum, g.act, g.slope);
         } else if (EPI == EPI_COUPLE_ADD) {
           g.out[p * g.ldo + n] = g.base[p * g.ldb + n] + round8(v);
         } else if (EPI == EPI_COUPLE_SUB) {
@@ -250,21 +275,40 @@ __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmArgs g) {
 }
 
 // ------------------------------------------------------------------ dispatch
-template <int BM, int BN, int WM, int WN, int MODE>
-static int launch_gemm_epi(const GemmArgs& a0, int epi, hipStream_t s) {
-  GemmArgs a = a0;
+template <int BM, int BN, int WM, int WN, int MODE, int EPI>
+static int launch_one(GemmArgs a, hipStream_t s) {
   a.m_tiles = (int)((a.P + BM - 1) / BM);
   a.n_tiles = (a.N + BN - 1) / BN;
   dim3 grid((unsigned)(a.m_tiles * a.n_tiles));
-  switch (epi) {
-    case EPI_STORE: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, MODE, EPI_STORE>), grid, dim3(256), 0, s, a); break;
-    case EPI_ACT: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, MODE, EPI_ACT>), grid, dim3(256), 0, s, a); break;
-    case EPI_COUPLE_ADD: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, MODE, EPI_COUPLE_ADD>), grid, dim3(256), 0, s, a); break;
-    case EPI_COUPLE_SUB: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, MODE, EPI_COUPLE_SUB>), grid, dim3(256), 0, s, a); break;
-    case EPI_PRIOR: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, MODE, EPI_PRIOR>), grid, dim3(256), 0, s, a); break;
-    default: return IDF_ERR_ARG;
-  }
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, MODE, EPI>), grid, dim3(256), 0, s, a);
   return idf_last_error();
+}
+
+// Row-tile height: the largest BM whose grid still has >= 4 blocks per CU (1024),
+// else the smallest.  BM only changes how rows are grouped into blocks; every
+// output's k-order (and so its bits) is identical for any BM.
+template <int BN, int MODE, int EPI>
+static int launch_bn(const GemmArgs& a, hipStream_t s) {
+  const int64_t nt = (a.N + BN - 1) / BN;
+  auto blocks = [&](int bm) { return ((a.P + bm - 1) / bm) * nt; };
+  if (BN == 128) {
+    if (blocks(128) >= 1024) return launch_one<128, 128, 2, 2, MODE, EPI>(a, s);
+    return launch_one<64, 128, 1, 4, MODE, EPI>(a, s);
+  }
+  if (blocks(256) >= 1024) return launch_one<256, BN, 4, 1, MODE, EPI>(a, s);
+  if (blocks(128) >= 1024) return launch_one<128, BN, 4, 1, MODE, EPI>(a, s);
+  return launch_one<64, BN, 4, 1, MODE, EPI>(a, s);
+}
+
+template <int MODE, int EPI>
+static int launch_epi(const GemmArgs& a, int bn, hipStream_t s) {
+  switch (bn) {
+    case 16: return launch_bn<16, MODE, EPI>(a, s);
+    case 32: return launch_bn<32, MODE, EPI>(a, s);
+    case 48: return launch_bn<48, MODE, EPI>(a, s);
+    case 64: return launch_bn<64, MODE, EPI>(a, s);
+    default: return launch_bn<128, MODE, EPI>(a, s);
+  }
 }
 
 // Tile width for N output columns (shared with idfcodec/packing.py: tile_n()).
@@ -284,21 +328,18 @@ static int launch_gemm(const GemmArgs& a, int mode, int epi, int n_alloc, hipStr
   int bn = tile_n(a.N);
   if (n_alloc < ((a.N + bn - 1) / bn) * bn) return IDF_ERR_ARG;
   if (mode == MODE_DENSE) {
-    switch (bn) {
-      case 16: return launch_gemm_epi<256, 16, 4, 1, MODE_DENSE>(a, epi, s);
-      case 32: return launch_gemm_epi<256, 32, 4, 1, MODE_DENSE>(a, epi, s);
-      case 48: return launch_gemm_epi<256, 48, 4, 1, MODE_DENSE>(a, epi, s);
-      case 64: return launch_gemm_epi<256, 64, 4, 1, MODE_DENSE>(a, epi, s);
-      default: return launch_gemm_epi<128, 128, 2, 2, MODE_DENSE>(a, epi, s);
+    switch (epi) {
+      case EPI_STORE: return launch_epi<MODE_DENSE, EPI_STORE>(a, bn, s);
+      case EPI_COUPLE_ADD: return launch_epi<MODE_DENSE, EPI_COUPLE_ADD>(a, bn, s);
+      case EPI_COUPLE_SUB: return launch_epi<MODE_DENSE, EPI_COUPLE_SUB>(a, bn, s);
+      case EPI_PRIOR: return launch_epi<MODE_DENSE, EPI_PRIOR>(a, bn, s);
+      default: return IDF_ERR_ARG;
     }
-  } else {
-    switch (bn) {
-      case 16: return launch_gemm_epi<256, 16, 4, 1, MODE_CONV3>(a, epi, s);
-      case 32: return launch_gemm_epi<256, 32, 4, 1, MODE_CONV3>(a, epi, s);
-      case 48: return launch_gemm_epi<256, 48, 4, 1, MODE_CONV3>(a, epi, s);
-      case 64: return launch_gemm_epi<256, 64, 4, 1, MODE_CONV3>(a, epi, s);
-      default: return launch_gemm_epi<128, 128, 2, 2, MODE_CONV3>(a, epi, s);
-    }
+  }
+  switch (epi) {
+    case EPI_ACT: return launch_epi<MODE_CONV3, EPI_ACT>(a, bn, s);
+    case EPI_ACT_FOLD: return launch_epi<MODE_CONV3, EPI_ACT_FOLD>(a, bn, s);
+    default: return IDF_ERR_ARG;
   }
 }
 
@@ -480,6 +521,18 @@ int idf_conv3x3_f32(void* stream, int32_t B, int32_t H, int32_t W, int32_t C, co
   return launch_gemm(g, MODE_CONV3, EPI_ACT, n_alloc, (hipStream_t)stream);
 }
 
+int idf_conv3x3_fold_f32(void* stream, int32_t B, int32_t H, int32_t W, int32_t C, const float* x,
+                         int64_t ld_x, const float* w, int32_t ldw, int32_t n_alloc,
+                         const float* b3, const float* vtap, int32_t ldv, const float* bfull,
+                         int32_t N, float* out, int64_t ld_out, int32_t act, float slope) {
+  if (!vtap || !bfull || ldv < N) return IDF_ERR_ARG;
+  GemmArgs g = {};
+  g.P = (int64_t)B * H * W; g.K = C; g.N = N; g.A = x; g.lda = ld_x; g.W = w; g.ldw = ldw;
+  g.bias = b3; g.out = out; g.ldo = ld_out; g.B = B; g.H = H; g.Wd = W; g.act = act;
+  g.slope = slope; g.vtap = vtap; g.bfull = bfull; g.ldv = ldv;
+  return launch_gemm(g, MODE_CONV3, EPI_ACT_FOLD, n_alloc, (hipStream_t)stream);
+}
+
 }  // extern "C"
 
 // ------------------------------------------------------------------ timer
@@ -518,6 +571,16 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
   for (int i = 0; i < blk->depth; ++i) {
     const int c = blk->k_in[i];
     const double cr = blk->c_real[i], gr = blk->g_real[i];
+    if (blk->fold) {  // one launch per layer: 3x3 over the layer input, 1x1 folded in
+      timer_mark(timer, s, IDF_TAG_CONV3X3, 2.0 * P * 9.0 * cr * gr, true);
+      int rc = idf_conv3x3_fold_f32(stream, B, H, W, c, feat, ld_feat, blk->w3[i], blk->ldw3[i],
+                                    blk->g_alloc, blk->b3[i], blk->vtap[i], blk->ldv,
+                                    blk->bfull[i], blk->g_pad, feat + c, ld_feat, blk->act,
+                                    blk->slope);
+      timer_mark(timer, s, 0, 0, false);
+      if (rc) return rc;
+      continue;
+    }
     timer_mark(timer, s, IDF_TAG_CONV1X1, 2.0 * P * cr * cr, true);
     int rc = idf_conv1x1_f32(stream, P, c, c, feat, ld_feat, blk->w1[i], blk->ldw1[i],
                              blk->n1_alloc[i], blk->b1[i], tmp, ld_tmp, B, H, W, nullptr);

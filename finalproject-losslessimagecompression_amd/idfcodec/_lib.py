@@ -50,6 +50,7 @@ class IdfDenseBlock(ctypes.Structure):
         ("w3", P * MAX_DEPTH), ("b3", P * MAX_DEPTH), ("n_head", i32), ("nh_alloc", i32),
         ("ldwh", i32), ("wh", P), ("bh", P),
         ("c_real", i32 * (MAX_DEPTH + 1)), ("g_real", i32 * MAX_DEPTH),
+        ("fold", i32), ("ldv", i32), ("vtap", P * MAX_DEPTH), ("bfull", P * MAX_DEPTH),
     ]
 
 
@@ -83,6 +84,8 @@ SIGNATURES = {
                                        i32, P]),
     "idf_conv3x3_f32": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, i32, P, i32, P, i64,
                                        i32, f32]),
+    "idf_conv3x3_fold_f32": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, i32, P, P, i32,
+                                            P, i32, P, i64, i32, f32]),
     "idf_dequant_u8": (ctypes.c_int, [P, i32, i32, i32, i32, P, P, i64]),
     "idf_quant_u8": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, P]),
     "idf_squeeze": (ctypes.c_int, [P, i32, i32, i32, i32, i32, P, i64, P, i64]),

@@ -17,6 +17,7 @@ HBM layout (per batch of B images):
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -27,6 +28,9 @@ from ._lib import IdfDenseBlock, IdfHeadOut, check, lib, ptr
 from .packing import PackedBlock, pack_dense_block, round_up
 
 FLOAT = 4
+# Fold each DenseLayer's 1x1 conv into its 3x3 conv (packing.fold_layer): -46% of the
+# flow FLOPs at imagenet64; IDF_FOLD=0 runs the reference's two convolutions instead.
+FOLD = os.environ.get("IDF_FOLD", "1") != "0"
 
 
 class DeviceBlock:
@@ -42,6 +46,8 @@ class DeviceBlock:
         self.b3 = [dev(a) for a in packed.b3]
         self.wh = dev(packed.wh)
         self.bh = dev(packed.bh)
+        self.vtap = [dev(a) for a in packed.vtap]
+        self.bfull = [dev(a) for a in packed.bfull]
         d = IdfDenseBlock()
         g = self.geom
         d.depth = g.depth
@@ -70,6 +76,11 @@ class DeviceBlock:
             d.g_real[i] = g.growth[i]
             c += g.growth[i]
         d.c_real[g.depth] = c
+        d.fold = 1 if packed.fold else 0
+        d.ldv = packed.g_alloc
+        for i in range(len(self.vtap)):
+            d.vtap[i] = self.vtap[i].data_ptr()
+            d.bfull[i] = self.bfull[i].data_ptr()
         self.desc = d
         self.timer = None  # an IdfTimer handle: when set, GEMM launches are event-timed
 
@@ -125,8 +136,9 @@ class FlowEngine:
     """Built from a model exposing the reference attributes/state_dict
     (IDFlows / ConditionalFlows of this package)."""
 
-    def __init__(self, model, device=None):
+    def __init__(self, model, device=None, fold: bool | None = None):
         self.device = torch.device(device or "cuda")
+        self.fold = FOLD if fold is None else bool(fold)
         sd = {k: v for k, v in model.state_dict().items()}
         self.conditional = type(model).__name__ == "ConditionalFlows"
         self.conv_for_cond = bool(getattr(model, "conv_for_cond", False))
@@ -163,10 +175,10 @@ class FlowEngine:
         self.inv_ids = []
         for l in range(self.nsplit):
             self.couple.append([DeviceBlock(pack_dense_block(
-                sd, f"blocks.{l}.flows.{2 * k + 1}.dense.", c_depth, c_act), self.device)
-                for k in range(self.nflows)])
+                sd, f"blocks.{l}.flows.{2 * k + 1}.dense.", c_depth, c_act, fold=self.fold),
+                self.device) for k in range(self.nflows)])
             self.prior.append(DeviceBlock(pack_dense_block(sd, f"blocks.{l}.prior.NN.", p_depth,
-                                                           p_act), self.device))
+                                                           p_act, fold=self.fold), self.device))
             ids_l, inv_l = [], []
             for k in range(self.nflows + 1):
                 Pm = sd[f"blocks.{l}.flows.{2 * k}.P"].detach().float().cpu()
@@ -197,13 +209,14 @@ class FlowEngine:
         offs.append(o)
         return offs
 
-    def flops_per_image(self) -> dict:
-        """algorithmic FLOPs of one image per direction (unpadded, as the reference)"""
+    def flops_per_image(self, fold: bool = False) -> dict:
+        """FLOPs of one image per direction (unpadded): fold=False as the reference
+        computes the flow; fold=True as this engine does when it folds the 1x1 convs."""
         c = p = 0
         for l, L in enumerate(self.levels):
             hw = L.h * L.w
-            c += hw * sum(b.geom.flops_per_pixel() for b in self.couple[l])
-            p += hw * self.prior[l].geom.flops_per_pixel()
+            c += hw * sum(b.geom.flops_per_pixel(fold) for b in self.couple[l])
+            p += hw * self.prior[l].geom.flops_per_pixel(fold)
         return {"couple": c, "prior": p, "total": c + p}
 
     # ------------------------------------------------------------ workspace

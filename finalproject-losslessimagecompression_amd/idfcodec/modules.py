@@ -21,14 +21,17 @@ def _param_key(module):
     return tuple((p.data_ptr(), p._version) for p in module.parameters())
 
 
-def device_block(block, device) -> DeviceBlock:
-    """Packed DeviceBlock of a DenseBlock module, cached until its parameters change."""
-    key = (_param_key(block), str(device))
+def device_block(block, device, fold=None) -> DeviceBlock:
+    """Packed DeviceBlock of a DenseBlock module, cached until its parameters change.
+    fold: fold the 1x1 convs into the 3x3 convs (default: engine.FOLD)."""
+    from .engine import FOLD
+    fold = FOLD if fold is None else bool(fold)
+    key = (_param_key(block), str(device), fold)
     cached = getattr(block, "_idf_device_block", None)
     if cached is not None and cached[0] == key:
         return cached[1]
     sd = {k: v for k, v in block.state_dict().items()}
-    db = DeviceBlock(pack_dense_block(sd, "", block.depth, block.act_name), device)
+    db = DeviceBlock(pack_dense_block(sd, "", block.depth, block.act_name, fold=fold), device)
     object.__setattr__(block, "_idf_device_block", (key, db))
     return db
 
@@ -60,10 +63,10 @@ def _feat_from_nchw(x, db: DeviceBlock, extra_cols=0):
 
 
 @torch.no_grad()
-def run_dense_block(block, x: torch.Tensor) -> torch.Tensor:
+def run_dense_block(block, x: torch.Tensor, fold=None) -> torch.Tensor:
     """DenseBlock.forward (nnblock.py:53-56) -> NCHW [B, o_channel, H, W]."""
     require_device(x, "DenseBlock input")
-    db = device_block(block, x.device)
+    db = device_block(block, x.device, fold)
     B, C, H, W = x.shape
     feat, ld, s = _feat_from_nchw(x, db)
     tmp = torch.empty_like(feat)

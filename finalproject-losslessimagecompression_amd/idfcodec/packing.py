@@ -79,12 +79,13 @@ class BlockGeometry:
     def positions(self, n: int) -> np.ndarray:
         return np.array([self.pos(c) for c in range(n)], dtype=np.int64)
 
-    def flops_per_pixel(self) -> int:
-        """algorithmic FLOPs of the block per pixel (unpadded, as the reference)"""
+    def flops_per_pixel(self, fold: bool = False) -> int:
+        """algorithmic FLOPs of the block per pixel (unpadded).  fold=False: as the
+        reference computes it; fold=True: with each 1x1 folded into its 3x3."""
         f = 0
         c = self.a
         for g in self.growth:
-            f += 2 * c * c + 2 * 9 * c * g
+            f += (0 if fold else 2 * c * c) + 2 * 9 * c * g
             c += g
         return f + 2 * c * self.n_head
 
@@ -94,6 +95,9 @@ class PackedBlock:
     geom: BlockGeometry
     act: str
     slope: float
+    fold: bool
+    vtap: list           # fold: [9][g_alloc] per-tap 1x1 bias through W3 (else empty)
+    bfull: list          # fold: [g_alloc] b3 + sum_tap vtap (fp32, tap order)
     w1: list[np.ndarray]
     b1: list[np.ndarray]
     w3: list[np.ndarray]
@@ -108,10 +112,33 @@ class PackedBlock:
     ldwh: int
 
 
+def fold_layer(w1, b1, w3):
+    """Fold a DenseLayer's 1x1 conv into its 3x3 conv (nnlayer.py:42-51).
+
+    conv3x3(pad0(W1 x + b1)) = sum_tap W3[tap] W1 x[nbr] + sum_{tap in image} W3[tap] b1,
+    exactly, because the reference zero-pads the 1x1 OUTPUT.  Returns
+    wf[g, tap, c] = sum_o W3[g, o, tap] W1[o, c] and v[tap, g] = sum_o W3[g, o, tap] b1[o],
+    both formed in float64 and rounded once to float32."""
+    w3t = w3.reshape(w3.shape[0], w3.shape[1], 9).astype(np.float64)      # [g, o, tap]
+    wf = np.einsum("got,oc->gtc", w3t, w1.astype(np.float64))
+    v = np.einsum("got,o->tg", w3t, b1.astype(np.float64))
+    return wf.astype(np.float32), v.astype(np.float32)
+
+
+def interior_bias(b3: np.ndarray, v: np.ndarray) -> np.ndarray:
+    """b3 + v[0] + ... + v[8], sequential fp32 adds: the order the device's border
+    loop uses, so interior and border pixels see the same arithmetic."""
+    s = b3.astype(np.float32).copy()
+    for t in range(9):
+        s = (s + v[t]).astype(np.float32)
+    return s
+
+
 def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
-                     slope: float = 0.01) -> PackedBlock:
+                     slope: float = 0.01, fold: bool = False) -> PackedBlock:
     """Pack the reference DenseBlock parameters found under `prefix` in `sd`
-    (keys `{prefix}layers.{i}.layers.{0,1}.{weight,bias}`, head `{prefix}layers.{depth}.*`)."""
+    (keys `{prefix}layers.{i}.layers.{0,1}.{weight,bias}`, head `{prefix}layers.{depth}.*`).
+    fold=True folds each layer's 1x1 conv into its 3x3 conv (fold_layer)."""
     def arr(k):
         v = sd[prefix + k]
         if hasattr(v, "detach"):
@@ -126,6 +153,7 @@ def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
     geom = BlockGeometry(a=a, depth=depth, growth=gs, n_head=n_head)
     g_alloc = round_up(geom.g_pad, tile_n(geom.g_pad))
     w1s, b1s, w3s, b3s, n1s, ld1s, ld3s = [], [], [], [], [], [], []
+    vts, bfs = [], []
     c = a
     for i in range(depth):
         k = geom.k_in[i]
@@ -144,10 +172,18 @@ def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
         ldw3 = round_up(k, 16)
         w3p = np.zeros((g_alloc, 9, ldw3), np.float32)
         g = w3.shape[0]
-        # [g, c, ky, kx] -> [g, tap=ky*3+kx, pos(c)]
-        w3p[:g][:, :, pos] = w3.reshape(g, c, 9).transpose(0, 2, 1)
         b3p = np.zeros(g_alloc, np.float32)
         b3p[:g] = b3
+        if fold:
+            wf, v = fold_layer(w1, b1, w3)
+            w3p[:g][:, :, pos] = wf
+            vp = np.zeros((9, g_alloc), np.float32)
+            vp[:, :g] = v
+            vts.append(vp)
+            bfs.append(interior_bias(b3p, vp))
+        else:
+            # [g, c, ky, kx] -> [g, tap=ky*3+kx, pos(c)]
+            w3p[:g][:, :, pos] = w3.reshape(g, c, 9).transpose(0, 2, 1)
         w1s.append(w1p); b1s.append(b1p); w3s.append(w3p); b3s.append(b3p)
         n1s.append(n1_alloc); ld1s.append(ldw1); ld3s.append(ldw3)
         c += g
@@ -158,8 +194,8 @@ def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
     whp[:n_head][:, geom.positions(c)] = wh_src[:, :, 0, 0]
     bhp = np.zeros(nh_alloc, np.float32)
     bhp[:n_head] = arr(f"layers.{depth}.bias")
-    return PackedBlock(geom, act, slope, w1s, b1s, w3s, b3s, whp, bhp, g_alloc, n1s, ld1s, ld3s,
-                       nh_alloc, ldwh)
+    return PackedBlock(geom, act, slope, fold, vts, bfs, w1s, b1s, w3s, b3s, whp, bhp, g_alloc,
+                       n1s, ld1s, ld3s, nh_alloc, ldwh)
 
 
 def unpack_features(feat: np.ndarray, geom: BlockGeometry, n: int) -> np.ndarray:

@@ -142,6 +142,14 @@ typedef struct IdfDenseBlock {
   const float *bh;
   int32_t c_real[IDF_MAX_DEPTH + 1];   /* unpadded input channels of layer i / head   */
   int32_t g_real[IDF_MAX_DEPTH];       /* unpadded growth of layer i                  */
+  /* fold = 1: layer i is ONE 3x3 conv over the layer input with the 1x1 conv
+   * folded in (w3[i] = W3[tap].W1, packed as above; w1/b1 unused); the 1x1 bias
+   * enters per valid tap: bias(p) = b3 + sum_{tap in image} vtap[i][tap*ldv + n],
+   * bfull[i][n] = that sum for interior pixels (same fp32 order). */
+  int32_t fold;
+  int32_t ldv;
+  const float *vtap[IDF_MAX_DEPTH];
+  const float *bfull[IDF_MAX_DEPTH];
 } IdfDenseBlock;
 
 /* Head epilogue target */
@@ -199,6 +207,15 @@ int idf_conv3x3_f32(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, co
                     int64_t ld_t, const float *d_w, int32_t ldw, int32_t n_alloc,
                     const float *d_bias, int32_t N, float *d_out, int64_t ld_out, int32_t act,
                     float slope);
+
+/* DenseLayer with the 1x1 conv folded into the 3x3 (see IdfDenseBlock.fold):
+ * out[p, n] = act(bias(p, n) + sum_{tap,c} X[nbr(p,tap), c] W[n, tap, c]), X = the layer
+ * INPUT; replaces nnlayer.py:42-51 (conv1x1 -> conv3x3 -> act) in one launch. */
+int idf_conv3x3_fold_f32(void *stream, int32_t B, int32_t H, int32_t W, int32_t C,
+                         const float *d_x, int64_t ld_x, const float *d_w, int32_t ldw,
+                         int32_t n_alloc, const float *d_b3, const float *d_vtap, int32_t ldv,
+                         const float *d_bfull, int32_t N, float *d_out, int64_t ld_out,
+                         int32_t act, float slope);
 
 /* ---- index maps (exact copies; no arithmetic) ---------------------------- */
 /* trainer.py:101 dequant of uint8 NCHW images to the 1/256 grid, written pixel-major:

@@ -189,11 +189,13 @@ def flow_fixture(name, cfg, B=2):
     out.update(sd_arrays(model))
     blocks_io = []
 
-    def hook(mod, inp, outp):
-        if len(blocks_io) < 4:
-            blocks_io.append((inp[0].detach().clone(), outp.detach().clone()))
+    def make_hook(name):
+        def hook(mod, inp, outp):
+            if len(blocks_io) < 4:
+                blocks_io.append((name, inp[0].detach().clone(), outp.detach().clone()))
+        return hook
 
-    hooks = [m.register_forward_hook(hook) for _, m in model.named_modules()
+    hooks = [m.register_forward_hook(make_hook(n)) for n, m in model.named_modules()
              if type(m).__name__ == "DenseBlock"]
     with torch.no_grad():
         if cfg["name"] == "ConditionalFlows":
@@ -210,7 +212,8 @@ def flow_fixture(name, cfg, B=2):
             h.remove()
         logp, logps = model.log_likelihood(lat, means, logs)
         gen = model.generated_from_latents(lat)
-    for i, (a, b) in enumerate(blocks_io):
+    for i, (nm, a, b) in enumerate(blocks_io):
+        out[f"dense{i}/name"] = np.frombuffer(nm.encode(), np.uint8)
         out[f"dense{i}/in"] = a.numpy()
         out[f"dense{i}/out"] = b.numpy()
     for i in range(len(lat)):

@@ -31,8 +31,10 @@ def _enc_streams(off, x, mean, scale, init=None):
     words = torch.empty(max(nsym, 1), dtype=torch.int32, device=dev)
     wb = lib().idf_rans_encode_workspace_bytes(nsym)
     ws = torch.empty(wb, dtype=torch.uint8, device=dev)
-    check(lib().idf_rans_encode_streams(_lib.stream_ptr(), ns, nsym, ptr(off_t), ptr(t(x)), ptr(t(mean)),
-                                        ptr(t(scale)), ptr(init_t), ptr(fs), ptr(words), ptr(nw),
+    # keep every device buffer referenced until the kernels have run
+    dx, dm, ds = t(x), t(mean), t(scale)
+    check(lib().idf_rans_encode_streams(_lib.stream_ptr(), ns, nsym, ptr(off_t), ptr(dx), ptr(dm),
+                                        ptr(ds), ptr(init_t), ptr(fs), ptr(words), ptr(nw),
                                         ptr(st), ptr(ws), wb), "enc")
     torch.cuda.synchronize()
     return (fs.cpu().numpy().view(np.uint64), words.cpu().numpy().view(np.uint32),
@@ -49,10 +51,10 @@ def _dec_streams(off, woff, nw, words, mean, scale, init):
     out = torch.empty(max(int(off[-1]), 1), dtype=torch.float32, device=dev)
     st = torch.empty(ns, dtype=torch.int32, device=dev)
     w = t(np.asarray(words, np.uint32).view(np.int32) if len(words) else np.zeros(1, np.int32), torch.int32)
-    check(lib().idf_rans_decode_streams(_lib.stream_ptr(), ns, ptr(t(off, torch.int64)),
-                                        ptr(t(woff, torch.int64)), ptr(t(nw, torch.int64)), ptr(w),
-                                        ptr(t(mean, torch.float32)), ptr(t(scale, torch.float32)),
-                                        ptr(t(np.asarray(init, np.uint64).view(np.int64), torch.int64)),
+    bufs = [t(off, torch.int64), t(woff, torch.int64), t(nw, torch.int64), w,
+            t(mean, torch.float32), t(scale, torch.float32),
+            t(np.asarray(init, np.uint64).view(np.int64), torch.int64)]
+    check(lib().idf_rans_decode_streams(_lib.stream_ptr(), ns, *[ptr(b) for b in bufs],
                                         ptr(fs), ptr(out), ptr(st)), "dec")
     torch.cuda.synchronize()
     return fs.cpu().numpy().view(np.uint64), out.cpu().numpy()[: int(off[-1])], st.cpu().numpy()
@@ -155,9 +157,9 @@ def test_device_cdf_matches_oracle(oracle):
     dev = torch.device("cuda")
     st = torch.empty(n, dtype=torch.int32, device=dev)
     fr = torch.empty(n, dtype=torch.int32, device=dev)
-    t = lambda a: torch.from_numpy(a).to(dev)  # noqa
-    check(lib().idf_rans_cdf_freq(_lib.stream_ptr(), n, ptr(t(x)), ptr(t(mean)), ptr(t(scale)), ptr(st),
-                                  ptr(fr)), "cdf")
+    dx, dm, ds = (torch.from_numpy(a).to(dev) for a in (x, mean, scale))
+    check(lib().idf_rans_cdf_freq(_lib.stream_ptr(), n, ptr(dx), ptr(dm), ptr(ds), ptr(st), ptr(fr)),
+          "cdf")
     rst, rfr = oracle.cdf_freq(x, mean, scale)
     assert np.array_equal(st.cpu().numpy(), rst) and np.array_equal(fr.cpu().numpy(), rfr)
 
