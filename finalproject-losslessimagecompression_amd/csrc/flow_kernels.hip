@@ -150,8 +150,11 @@ __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmArgs g) {
   auto load_chunk = [&](int kc) {
     int tap = 0, c0 = kc * BK;
     if (MODE == MODE_CONV3) {
-      tap = kc / nkc;
-      c0 = (kc - tap * nkc) * BK;
+      // channel-major, tap-minor: the 9 taps of one 16-channel slab are consecutive
+      // chunks, so a slab's 9 shifted re-reads hit L1/L2 instead of HBM
+      const int slab = kc / 9;
+      tap = kc - slab * 9;
+      c0 = slab * BK;
     }
 #pragma unroll
     for (int j = 0; j < A_PER_T; ++j) {
@@ -573,10 +576,15 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
     const double cr = blk->c_real[i], gr = blk->g_real[i];
     if (blk->fold) {  // one launch per layer: 3x3 over the layer input, 1x1 folded in
       timer_mark(timer, s, IDF_TAG_CONV3X3, 2.0 * P * 9.0 * cr * gr, true);
-      int rc = idf_conv3x3_fold_f32(stream, B, H, W, c, feat, ld_feat, blk->w3[i], blk->ldw3[i],
-                                    blk->g_alloc, blk->b3[i], blk->vtap[i], blk->ldv,
-                                    blk->bfull[i], blk->g_pad, feat + c, ld_feat, blk->act,
-                                    blk->slope);
+      int rc = blk->halo
+                   ? idf_conv3x3_halo(stream, B, H, W, c, feat, ld_feat, blk->w3[i], blk->ldw3[i],
+                                      blk->g_alloc, blk->b3[i], blk->vtap[i], blk->ldv,
+                                      blk->bfull[i], blk->g_pad, feat + c, ld_feat, blk->act,
+                                      blk->slope, tmp, P * ld_tmp)
+                   : idf_conv3x3_fold_f32(stream, B, H, W, c, feat, ld_feat, blk->w3[i],
+                                          blk->ldw3[i], blk->g_alloc, blk->b3[i], blk->vtap[i],
+                                          blk->ldv, blk->bfull[i], blk->g_pad, feat + c, ld_feat,
+                                          blk->act, blk->slope);
       timer_mark(timer, s, 0, 0, false);
       if (rc) return rc;
       continue;

@@ -31,6 +31,9 @@ FLOAT = 4
 # Fold each DenseLayer's 1x1 conv into its 3x3 conv (packing.fold_layer): -46% of the
 # flow FLOPs at imagenet64; IDF_FOLD=0 runs the reference's two convolutions instead.
 FOLD = os.environ.get("IDF_FOLD", "1") != "0"
+# Folded 3x3 convs run on the LDS halo-tiled kernel (conv3_halo.hip); IDF_HALO=0 selects
+# the implicit-GEMM kernel instead (A/B comparisons).
+HALO = os.environ.get("IDF_HALO", "1") != "0"
 
 
 class DeviceBlock:
@@ -77,6 +80,7 @@ class DeviceBlock:
             c += g.growth[i]
         d.c_real[g.depth] = c
         d.fold = 1 if packed.fold else 0
+        d.halo = 1 if (packed.fold and HALO) else 0
         d.ldv = packed.g_alloc
         for i in range(len(self.vtap)):
             d.vtap[i] = self.vtap[i].data_ptr()

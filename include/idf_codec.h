@@ -150,6 +150,9 @@ typedef struct IdfDenseBlock {
   int32_t ldv;
   const float *vtap[IDF_MAX_DEPTH];
   const float *bfull[IDF_MAX_DEPTH];
+  /* halo = 1 (with fold = 1): the folded 3x3 runs as idf_conv3x3_halo, using the
+   * block's tmp buffer as split-K workspace; 0: the implicit-GEMM kernel */
+  int32_t halo;
 } IdfDenseBlock;
 
 /* Head epilogue target */
@@ -216,6 +219,18 @@ int idf_conv3x3_fold_f32(void *stream, int32_t B, int32_t H, int32_t W, int32_t 
                          int32_t n_alloc, const float *d_b3, const float *d_vtap, int32_t ldv,
                          const float *d_bfull, int32_t N, float *d_out, int64_t ld_out,
                          int32_t act, float slope);
+
+/* The same 3x3 conv as an LDS halo-tiled kernel (the hot path): per 16-channel
+ * slab, a tile's (rows+2) x (cols+2) neighbourhood is staged in LDS once and read
+ * by all 9 taps.  d_vtap == NULL: plain bias d_b3 (no fold).  Small images split
+ * the channel reduction (fixed by H, W, C -- never B) into partial sums kept in
+ * d_workspace (idf_conv3x3_halo_workspace floats; may be NULL when that is 0). */
+int64_t idf_conv3x3_halo_workspace(int32_t B, int32_t H, int32_t W, int32_t C, int32_t N);
+int idf_conv3x3_halo(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, const float *d_x,
+                     int64_t ld_x, const float *d_w, int32_t ldw, int32_t n_alloc,
+                     const float *d_b3, const float *d_vtap, int32_t ldv, const float *d_bfull,
+                     int32_t N, float *d_out, int64_t ld_out, int32_t act, float slope,
+                     float *d_workspace, int64_t workspace_floats);
 
 /* ---- index maps (exact copies; no arithmetic) ---------------------------- */
 /* trainer.py:101 dequant of uint8 NCHW images to the 1/256 grid, written pixel-major:

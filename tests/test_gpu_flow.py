@@ -175,3 +175,53 @@ def test_imagenet64_forward_vs_reference(golden):
     # theoretical bits per sub-pixel within 1% of the reference's
     assert abs(lp.mean().item() / d["log_prob"].mean() - 1) < 0.01
     del synthetic
+
+
+@pytest.mark.parametrize("B,H,W,C,N,act,fold", [
+    (3, 32, 32, 52, 44, "ReLU", True), (5, 16, 16, 100, 44, "ReLU", True),
+    (7, 8, 8, 168, 44, "ReLU", True), (2, 27, 23, 40, 32, "LeakyReLU", True),
+    (9, 4, 4, 24, 64, "ReLU", True), (4, 2, 2, 16, 128, "ReLU", False),
+    (1, 8, 8, 12, 44, "ReLU", False), (2, 64, 64, 8, 16, "ReLU", True)])
+def test_conv3x3_halo_kernel_vs_fp64(B, H, W, C, N, act, fold):
+    """The LDS halo-tiled 3x3 conv (incl. split-K for small images, ragged tiles,
+    several n-tiles) against an fp64 conv2d with the same padded weights."""
+    import torch.nn.functional as F
+    from idfcodec import _lib
+    from idfcodec._lib import check, lib, ptr
+    from idfcodec.packing import round_up, tile_n
+    g = torch.Generator().manual_seed(B * 1000 + H * 10 + C)
+    ld = round_up(C + N, 16) + 4
+    X = torch.randn(B * H * W, ld, generator=g)
+    ldw = round_up(C, 16)
+    n_alloc = round_up(N, 64)
+    Wt = torch.randn(n_alloc, 9, ldw, generator=g) * 0.05
+    b3 = torch.randn(n_alloc, generator=g) * 0.1
+    vt = torch.randn(9, n_alloc, generator=g) * 0.1 if fold else None
+    bfull = None
+    if fold:
+        s = b3.clone()
+        for t in range(9):
+            s = s + vt[t]
+        bfull = s
+    dev = torch.device("cuda")
+    Xd, Wd_, b3d = X.to(dev), Wt.to(dev), b3.to(dev)
+    vtd = vt.to(dev) if fold else None
+    bfd = bfull.to(dev) if fold else None
+    out = torch.zeros(B * H * W, ld, device=dev)
+    wsn = lib().idf_conv3x3_halo_workspace(B, H, W, C, N)
+    ws = torch.empty(max(wsn, 1), device=dev)
+    check(lib().idf_conv3x3_halo(_lib.stream_ptr(), B, H, W, C, ptr(Xd), ld, ptr(Wd_), ldw, n_alloc,
+                                 ptr(b3d), ptr(vtd), n_alloc, ptr(bfd), N, ptr(out), ld,
+                                 _lib.ACT[act], 0.01, ptr(ws), wsn), "halo")
+    torch.cuda.synchronize()
+    x4 = X[:, :C].double().view(B, H, W, C).permute(0, 3, 1, 2)
+    w4 = Wt[:N, :, :C].double().permute(0, 2, 1).reshape(N, C, 3, 3)
+    ref = F.conv2d(x4, w4, padding=1) + b3[:N].double().view(1, -1, 1, 1)
+    if fold:
+        mask = F.conv2d(torch.ones(1, 1, H, W, dtype=torch.float64),
+                        torch.eye(9, dtype=torch.float64).view(9, 1, 3, 3), padding=1)
+        ref = ref + torch.einsum("tn,bthw->bnhw", vt[:, :N].double(), mask)
+    ref = F.relu(ref) if act == "ReLU" else F.leaky_relu(ref, 0.01)
+    got = out[:, :N].cpu().double().view(B, H, W, N).permute(0, 3, 1, 2)
+    close(got, ref, 2e-5)
+    assert torch.all(out[:, N:].cpu() == 0), "wrote outside the N output columns"

@@ -20,7 +20,9 @@ for s in $STAGES; do
     tests) step gpu_tests 900 python -m pytest tests -m gpu -q -rf --durations=15 ;;
     fasttests) step gpu_tests 900 python -m pytest tests -m "gpu and not slow" -q -rf --durations=15 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    kbench) step kbench 300 python tools/kbench.py ;;
     bench) step bench 600 python bench.py ;;
+    bench_nofold) IDF_FOLD=0 step bench_nofold 600 python bench.py --no-cpu-baseline ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
           step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 ;;
   esac

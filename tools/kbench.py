@@ -1,0 +1,72 @@
+"""Kernel microbenchmark of the folded 3x3 conv at the imagenet64 shapes (B=256): the LDS
+halo-tiled kernel (idf_conv3x3_halo) and the implicit-GEMM kernel (idf_conv3x3_fold_f32),
+per level and layer width.  Prints achieved TFLOP/s (unpadded FLOPs)."""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "finalproject-losslessimagecompression_amd"))
+
+import torch  # noqa: E402
+
+from idfcodec import _lib  # noqa: E402
+from idfcodec._lib import check, lib, ptr  # noqa: E402
+from idfcodec.packing import round_up  # noqa: E402
+
+
+def time_it(fn, reps=10):
+    fn()
+    torch.cuda.synchronize()
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def main():
+    B = int(os.environ.get("KB_B", "256"))
+    dev = torch.device("cuda")
+    s = _lib.stream_ptr()
+    g_pad, g_alloc, g_real = 44, 48, 43
+    tot = {"halo": [0.0, 0.0], "gemm": [0.0, 0.0]}
+    for lvl, (hw, a) in enumerate(((32, 9), (16, 18), (8, 36))):
+        P = B * hw * hw
+        for layer in (0, 3, 6, 9, 11):
+            c_pad = round_up(a, 4) + layer * g_pad
+            c_real = a + layer * 512 // 12
+            ld = round_up(c_pad + g_pad, 16)
+            feat = torch.randn(P * ld, device=dev)
+            ldw = round_up(c_pad, 16)
+            w = torch.randn(g_alloc * 9 * ldw, device=dev) * 0.01
+            b3 = torch.zeros(g_alloc, device=dev)
+            vt = torch.zeros(9 * g_alloc, device=dev)
+            wsn = lib().idf_conv3x3_halo_workspace(B, hw, hw, c_pad, g_pad)
+            ws = torch.empty(max(wsn, 1), device=dev)
+            fl = 2.0 * P * 9 * c_real * g_real
+
+            def halo():
+                check(lib().idf_conv3x3_halo(s, B, hw, hw, c_pad, ptr(feat), ld, ptr(w), ldw, g_alloc,
+                                             ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
+                                             ptr(feat) + c_pad * 4, ld, 0, 0.0, ptr(ws), wsn), "halo")
+
+            def gemm():
+                check(lib().idf_conv3x3_fold_f32(s, B, hw, hw, c_pad, ptr(feat), ld, ptr(w), ldw,
+                                                 g_alloc, ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
+                                                 ptr(feat) + c_pad * 4, ld, 0, 0.0), "gemm")
+            line = f"L{lvl} hw={hw:2d} c={c_pad:4d} P={P:7d}"
+            for name, fn in (("halo", halo), ("gemm", gemm)):
+                ms = time_it(fn)
+                tot[name][0] += ms
+                tot[name][1] += fl
+                line += f"  {name} {ms*1e3:8.1f} us {fl/ms/1e9:6.1f} TF/s"
+            print(line, flush=True)
+    for k, (ms, fl) in tot.items():
+        print(f"{k}: sampled total {ms:.2f} ms  {fl/ms/1e9:.1f} TF/s")
+
+
+if __name__ == "__main__":
+    main()
