@@ -45,6 +45,16 @@ def parse():
     return ap.parse_args()
 
 
+def conv_kernel_name(eng):
+    from idfcodec import engine
+    if eng.fold and engine.HALO:
+        return ("conv3_halo_kernel<3> (+conv3_reduce_kernel at 8x8): DenseLayer 3x3 conv with "
+                "the 1x1 folded in, LDS halo tiles, f32 MFMA")
+    if eng.fold:
+        return "gemm_f32_kernel<BM,48,4,1,MODE_CONV3,EPI_ACT_FOLD> (folded 3x3 conv, implicit GEMM)"
+    return "gemm_f32_kernel<BM,48,4,1,MODE_CONV3,EPI_ACT> (3x3 conv, implicit GEMM)"
+
+
 def cpu_baseline(model_cfg, n_img):
     """The oracle on the host: torch-fp32 flow (oracle/flow_oracle.py) + C rANS
     (oracle/rans_oracle.c, OpenMP over streams), encode then decode of n_img images.
@@ -222,7 +232,9 @@ def main():
                 B * eng.flops_per_image(fold=eng.fold)["total"] / 1e12, 4),
             "fold_1x1_into_3x3": eng.fold,
             "roofline": {
-                "kernel": "gemm_f32_kernel<256,48,4,1,MODE_CONV3,EPI_ACT> (3x3 conv, implicit GEMM)",
+                "kernel": conv_kernel_name(eng),
+                "flops_per_launch": "2*P*9*c*g (P = B*h*w pixels, c/g unpadded in/out "
+                                    "channels of the layer; averaged over the sampled launches)",
                 "bound": "mfma",
                 "achieved": round(c3_tflops, 3),
                 "peak": PEAK_F32_TFLOPS,
