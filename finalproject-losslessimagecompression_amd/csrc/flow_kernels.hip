@@ -576,7 +576,13 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
     const double cr = blk->c_real[i], gr = blk->g_real[i];
     if (blk->fold) {  // one launch per layer: 3x3 over the layer input, 1x1 folded in
       timer_mark(timer, s, IDF_TAG_CONV3X3, 2.0 * P * 9.0 * cr * gr, true);
-      int rc = blk->halo
+      const bool wino = blk->wino && blk->wino_u[i] && idf_conv3x3_wino_supported(H, W);
+      int rc = wino
+                   ? idf_conv3x3_wino(stream, B, H, W, c, feat, ld_feat, blk->wino_u[i],
+                                      blk->wino_nft, blk->b3[i], blk->vtap[i], blk->ldv,
+                                      blk->bfull[i], blk->g_pad, feat + c, ld_feat, blk->act,
+                                      blk->slope, tmp, P * ld_tmp)
+               : blk->halo
                    ? idf_conv3x3_halo(stream, B, H, W, c, feat, ld_feat, blk->w3[i], blk->ldw3[i],
                                       blk->g_alloc, blk->b3[i], blk->vtap[i], blk->ldv,
                                       blk->bfull[i], blk->g_pad, feat + c, ld_feat, blk->act,

@@ -51,7 +51,7 @@ class IdfDenseBlock(ctypes.Structure):
         ("ldwh", i32), ("wh", P), ("bh", P),
         ("c_real", i32 * (MAX_DEPTH + 1)), ("g_real", i32 * MAX_DEPTH),
         ("fold", i32), ("ldv", i32), ("vtap", P * MAX_DEPTH), ("bfull", P * MAX_DEPTH),
-        ("halo", i32),
+        ("halo", i32), ("wino", i32), ("wino_nft", i32), ("wino_u", P * MAX_DEPTH),
     ]
 
 
@@ -90,6 +90,10 @@ SIGNATURES = {
     "idf_conv3x3_halo_workspace": (i64, [i32, i32, i32, i32, i32]),
     "idf_conv3x3_halo": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, i32, P, P, i32, P,
                                         i32, P, i64, i32, f32, P, i64]),
+    "idf_conv3x3_wino_supported": (ctypes.c_int, [i32, i32]),
+    "idf_conv3x3_wino_workspace": (i64, [i32, i32, i32, i32, i32]),
+    "idf_conv3x3_wino": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, P, P, i32, P, i32, P,
+                                        i64, i32, f32, P, i64]),
     "idf_dequant_u8": (ctypes.c_int, [P, i32, i32, i32, i32, P, P, i64]),
     "idf_quant_u8": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, P]),
     "idf_squeeze": (ctypes.c_int, [P, i32, i32, i32, i32, i32, P, i64, P, i64]),

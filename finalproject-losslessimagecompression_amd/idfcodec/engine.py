@@ -34,6 +34,9 @@ FOLD = os.environ.get("IDF_FOLD", "1") != "0"
 # Folded 3x3 convs run on the LDS halo-tiled kernel (conv3_halo.hip); IDF_HALO=0 selects
 # the implicit-GEMM kernel instead (A/B comparisons).
 HALO = os.environ.get("IDF_HALO", "1") != "0"
+# Folded 3x3 convs on even-sized images run as Winograd F(2x2,3x3) (conv3_wino.hip, 2.25x
+# fewer multiplies); IDF_WINO=0 keeps them on the direct halo kernel.
+WINO = os.environ.get("IDF_WINO", "1") != "0"
 
 
 class DeviceBlock:
@@ -51,6 +54,7 @@ class DeviceBlock:
         self.bh = dev(packed.bh)
         self.vtap = [dev(a) for a in packed.vtap]
         self.bfull = [dev(a) for a in packed.bfull]
+        self.wino_u = [dev(a) for a in packed.wino_u]
         d = IdfDenseBlock()
         g = self.geom
         d.depth = g.depth
@@ -81,6 +85,10 @@ class DeviceBlock:
         d.c_real[g.depth] = c
         d.fold = 1 if packed.fold else 0
         d.halo = 1 if (packed.fold and HALO) else 0
+        d.wino = 1 if (packed.fold and self.wino_u) else 0
+        d.wino_nft = packed.g_alloc // 16
+        for i, u in enumerate(self.wino_u):
+            d.wino_u[i] = u.data_ptr()
         d.ldv = packed.g_alloc
         for i in range(len(self.vtap)):
             d.vtap[i] = self.vtap[i].data_ptr()
@@ -143,6 +151,9 @@ class FlowEngine:
     def __init__(self, model, device=None, fold: bool | None = None):
         self.device = torch.device(device or "cuda")
         self.fold = FOLD if fold is None else bool(fold)
+        self.wino = self.fold and WINO and any(
+            lib().idf_conv3x3_wino_supported(model.H // s, model.W // s)
+            for s in [model.blocks[0]["extend"].scale ** (l + 1) for l in range(model.nsplit)])
         sd = {k: v for k, v in model.state_dict().items()}
         self.conditional = type(model).__name__ == "ConditionalFlows"
         self.conv_for_cond = bool(getattr(model, "conv_for_cond", False))
@@ -179,10 +190,12 @@ class FlowEngine:
         self.inv_ids = []
         for l in range(self.nsplit):
             self.couple.append([DeviceBlock(pack_dense_block(
-                sd, f"blocks.{l}.flows.{2 * k + 1}.dense.", c_depth, c_act, fold=self.fold),
+                sd, f"blocks.{l}.flows.{2 * k + 1}.dense.", c_depth, c_act, fold=self.fold,
+                wino=self.wino),
                 self.device) for k in range(self.nflows)])
             self.prior.append(DeviceBlock(pack_dense_block(sd, f"blocks.{l}.prior.NN.", p_depth,
-                                                           p_act, fold=self.fold), self.device))
+                                                           p_act, fold=self.fold, wino=self.wino),
+                                          self.device))
             ids_l, inv_l = [], []
             for k in range(self.nflows + 1):
                 Pm = sd[f"blocks.{l}.flows.{2 * k}.P"].detach().float().cpu()

@@ -110,6 +110,7 @@ class PackedBlock:
     ldw3: list[int]
     nh_alloc: int
     ldwh: int
+    wino_u: list = field(default_factory=list)  # fold+wino: wino_weights() per layer
 
 
 def fold_layer(w1, b1, w3):
@@ -119,10 +120,38 @@ def fold_layer(w1, b1, w3):
     exactly, because the reference zero-pads the 1x1 OUTPUT.  Returns
     wf[g, tap, c] = sum_o W3[g, o, tap] W1[o, c] and v[tap, g] = sum_o W3[g, o, tap] b1[o],
     both formed in float64 and rounded once to float32."""
+    wf, v = fold_layer64(w1, b1, w3)
+    return wf.astype(np.float32), v.astype(np.float32)
+
+
+def fold_layer64(w1, b1, w3):
+    """fold_layer before the final rounding (float64)."""
     w3t = w3.reshape(w3.shape[0], w3.shape[1], 9).astype(np.float64)      # [g, o, tap]
     wf = np.einsum("got,oc->gtc", w3t, w1.astype(np.float64))
     v = np.einsum("got,o->tg", w3t, b1.astype(np.float64))
-    return wf.astype(np.float32), v.astype(np.float32)
+    return wf, v
+
+
+# Winograd F(2x2, 3x3) weight transform (Lavin & Gray): U = G g G^T
+WINO_G = np.array([[1.0, 0.0, 0.0], [0.5, 0.5, 0.5], [0.5, -0.5, 0.5], [0.0, 0.0, 1.0]])
+
+
+def wino_weights(w: np.ndarray, nslab: int) -> np.ndarray:
+    """w: [n_alloc, 9, ldw] (float64 preferred) 3x3 weights in the padded channel
+    coordinates.  Returns U = G g G^T for every (n, c), rounded once to fp32 and laid out
+    in MFMA fragment order [16 positions][nslab][nft][64 lanes][4] (lane = 16*h + r holds
+    U[pos][16*f + r][16*slab + 4*h .. +3]) -- what conv3_wino.hip streams per wave."""
+    n_alloc = w.shape[0]
+    assert n_alloc % 16 == 0
+    nft = n_alloc // 16
+    C = nslab * 16
+    g = np.zeros((n_alloc, C, 3, 3), np.float64)
+    cw = min(C, w.shape[2])
+    g[:, :cw] = w[:, :, :cw].astype(np.float64).transpose(0, 2, 1).reshape(n_alloc, cw, 3, 3)
+    U = np.einsum("ai,ncij,bj->abnc", WINO_G, g, WINO_G).reshape(16, n_alloc, C)
+    U = U.reshape(16, nft, 16, nslab, 4, 4)          # pos, f, r, slab, h, e
+    U = U.transpose(0, 3, 1, 4, 2, 5)                 # pos, slab, f, h, r, e
+    return np.ascontiguousarray(U.reshape(16, nslab, nft, 64, 4).astype(np.float32))
 
 
 def interior_bias(b3: np.ndarray, v: np.ndarray) -> np.ndarray:
@@ -135,7 +164,7 @@ def interior_bias(b3: np.ndarray, v: np.ndarray) -> np.ndarray:
 
 
 def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
-                     slope: float = 0.01, fold: bool = False) -> PackedBlock:
+                     slope: float = 0.01, fold: bool = False, wino: bool = False) -> PackedBlock:
     """Pack the reference DenseBlock parameters found under `prefix` in `sd`
     (keys `{prefix}layers.{i}.layers.{0,1}.{weight,bias}`, head `{prefix}layers.{depth}.*`).
     fold=True folds each layer's 1x1 conv into its 3x3 conv (fold_layer)."""
@@ -153,7 +182,7 @@ def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
     geom = BlockGeometry(a=a, depth=depth, growth=gs, n_head=n_head)
     g_alloc = round_up(geom.g_pad, tile_n(geom.g_pad))
     w1s, b1s, w3s, b3s, n1s, ld1s, ld3s = [], [], [], [], [], [], []
-    vts, bfs = [], []
+    vts, bfs, wus = [], [], []
     c = a
     for i in range(depth):
         k = geom.k_in[i]
@@ -175,8 +204,13 @@ def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
         b3p = np.zeros(g_alloc, np.float32)
         b3p[:g] = b3
         if fold:
-            wf, v = fold_layer(w1, b1, w3)
+            wf64, v64 = fold_layer64(w1, b1, w3)
+            wf, v = wf64.astype(np.float32), v64.astype(np.float32)
             w3p[:g][:, :, pos] = wf
+            if wino:
+                w64 = np.zeros((g_alloc, 9, ldw3), np.float64)
+                w64[:g][:, :, pos] = wf64
+                wus.append(wino_weights(w64, ldw3 // 16))
             vp = np.zeros((9, g_alloc), np.float32)
             vp[:, :g] = v
             vts.append(vp)
@@ -195,7 +229,7 @@ def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
     bhp = np.zeros(nh_alloc, np.float32)
     bhp[:n_head] = arr(f"layers.{depth}.bias")
     return PackedBlock(geom, act, slope, fold, vts, bfs, w1s, b1s, w3s, b3s, whp, bhp, g_alloc,
-                       n1s, ld1s, ld3s, nh_alloc, ldwh)
+                       n1s, ld1s, ld3s, nh_alloc, ldwh, wus)
 
 
 def unpack_features(feat: np.ndarray, geom: BlockGeometry, n: int) -> np.ndarray:

@@ -153,6 +153,12 @@ typedef struct IdfDenseBlock {
   /* halo = 1 (with fold = 1): the folded 3x3 runs as idf_conv3x3_halo, using the
    * block's tmp buffer as split-K workspace; 0: the implicit-GEMM kernel */
   int32_t halo;
+  /* wino = 1 (with fold = 1): layers whose geometry idf_conv3x3_wino_supports run as
+   * Winograd F(2x2,3x3) with the transformed weights wino_u[i] (fragment order, see
+   * idf_conv3x3_wino); other geometries fall back to the halo kernel */
+  int32_t wino;
+  int32_t wino_nft;
+  const float *wino_u[IDF_MAX_DEPTH];
 } IdfDenseBlock;
 
 /* Head epilogue target */
@@ -231,6 +237,18 @@ int idf_conv3x3_halo(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, c
                      const float *d_b3, const float *d_vtap, int32_t ldv, const float *d_bfull,
                      int32_t N, float *d_out, int64_t ld_out, int32_t act, float slope,
                      float *d_workspace, int64_t workspace_floats);
+
+/* The same 3x3 conv as Winograd F(2x2, 3x3): 16 multiplies per 2x2 outputs instead
+ * of 36.  d_u holds U = G g G^T per (position, n, c), pre-arranged in MFMA fragment
+ * order [16 positions][ceil(C/16) slabs][nft n-fragments][64 lanes][4]
+ * (idfcodec/packing.py wino_weights).  Even H and W only (else IDF_ERR_UNSUPPORTED). */
+int idf_conv3x3_wino_supported(int32_t H, int32_t W);
+int64_t idf_conv3x3_wino_workspace(int32_t B, int32_t H, int32_t W, int32_t C, int32_t N);
+int idf_conv3x3_wino(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, const float *d_x,
+                     int64_t ld_x, const float *d_u, int32_t nft, const float *d_b3,
+                     const float *d_vtap, int32_t ldv, const float *d_bfull, int32_t N,
+                     float *d_out, int64_t ld_out, int32_t act, float slope, float *d_workspace,
+                     int64_t workspace_floats);
 
 /* ---- index maps (exact copies; no arithmetic) ---------------------------- */
 /* trainer.py:101 dequant of uint8 NCHW images to the 1/256 grid, written pixel-major:

@@ -32,7 +32,9 @@ def main():
     dev = torch.device("cuda")
     s = _lib.stream_ptr()
     g_pad, g_alloc, g_real = 44, 48, 43
-    tot = {"halo": [0.0, 0.0], "gemm": [0.0, 0.0]}
+    tot = {"wino": [0.0, 0.0], "halo": [0.0, 0.0], "gemm": [0.0, 0.0]}
+    import numpy as np
+    from idfcodec.packing import wino_weights
     for lvl, (hw, a) in enumerate(((32, 9), (16, 18), (8, 36))):
         P = B * hw * hw
         for layer in (0, 3, 6, 9, 11):
@@ -53,12 +55,22 @@ def main():
                                              ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
                                              ptr(feat) + c_pad * 4, ld, 0, 0.0, ptr(ws), wsn), "halo")
 
+            U = torch.from_numpy(wino_weights(np.random.default_rng(0).normal(
+                0, 0.01, (g_alloc, 9, ldw)), ldw // 16)).to(dev)
+            wwn = lib().idf_conv3x3_wino_workspace(B, hw, hw, c_pad, g_pad)
+            wws = torch.empty(max(wwn, 1), device=dev)
+
+            def wino():
+                check(lib().idf_conv3x3_wino(s, B, hw, hw, c_pad, ptr(feat), ld, ptr(U), g_alloc // 16,
+                                             ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
+                                             ptr(feat) + c_pad * 4, ld, 0, 0.0, ptr(wws), wwn), "wino")
+
             def gemm():
                 check(lib().idf_conv3x3_fold_f32(s, B, hw, hw, c_pad, ptr(feat), ld, ptr(w), ldw,
                                                  g_alloc, ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
                                                  ptr(feat) + c_pad * 4, ld, 0, 0.0), "gemm")
             line = f"L{lvl} hw={hw:2d} c={c_pad:4d} P={P:7d}"
-            for name, fn in (("halo", halo), ("gemm", gemm)):
+            for name, fn in (("wino", wino), ("halo", halo), ("gemm", gemm)):
                 ms = time_it(fn)
                 tot[name][0] += ms
                 tot[name][1] += fl
