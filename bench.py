@@ -47,12 +47,24 @@ def parse():
 
 def conv_kernel_name(eng):
     from idfcodec import engine
+    if eng.wino:
+        return ("conv3_wino_kernel<3> (+conv3_wino_reduce_kernel at 8x8): DenseLayer 3x3 conv "
+                "with the 1x1 folded in, Winograd F(2x2,3x3), f32 MFMA")
     if eng.fold and engine.HALO:
         return ("conv3_halo_kernel<3> (+conv3_reduce_kernel at 8x8): DenseLayer 3x3 conv with "
                 "the 1x1 folded in, LDS halo tiles, f32 MFMA")
     if eng.fold:
         return "gemm_f32_kernel<BM,48,4,1,MODE_CONV3,EPI_ACT_FOLD> (folded 3x3 conv, implicit GEMM)"
     return "gemm_f32_kernel<BM,48,4,1,MODE_CONV3,EPI_ACT> (3x3 conv, implicit GEMM)"
+
+
+def wino_exec_ratio(eng):
+    """MFMA FLOPs executed per algorithmic (direct-conv) FLOP of the 3x3 conv: Winograd
+    F(2x2,3x3) issues 16 products per 2x2 outputs instead of 36, over 16-padded outputs
+    (43 real growth channels -> 48).  1.0 for the direct kernels."""
+    if not eng.wino:
+        return 1.0
+    return 16.0 / 36.0 * 48.0 / 43.0
 
 
 def cpu_baseline(model_cfg, n_img):
@@ -242,6 +254,7 @@ def main():
                 "frac": round(c3_tflops / PEAK_F32_TFLOPS, 4),
                 "traffic": None,
                 "avg_launch_ms": round(c3_avg_ms, 5),
+                "mfma_executed_tflops": round(c3_tflops * wino_exec_ratio(eng), 3),
                 "conv1x1_achieved": round(c1_tflops, 3),
                 "conv1x1_avg_launch_ms": round(c1_avg_ms, 5),
             },

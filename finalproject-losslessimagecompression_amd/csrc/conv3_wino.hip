@@ -11,17 +11,20 @@
 //
 // Block = 8 waves, one spatial tile of up to 64 Winograd tiles (e.g. 8x32 output pixels
 // at 32x32, a whole 16x16 image, or four 8x8 images) x all N outputs of an n-tile.
-// Wave w owns transform positions 2w and 2w+1 (of 16) for all 64 tiles.  Per
-// 16-channel slab:
-//   * the tile's (rows+2) x (cols+2) halo of X is staged into LDS once, columns
-//     de-interleaved (even columns, then odd) so the stride-2 patch reads of 16
-//     neighbouring tiles are unit-stride, conflict-free ds_read_b128s;
-//   * each wave builds its V fragments on the fly (4 LDS reads + 3 vector adds per
-//     16 tiles x 4 channels) -- V never touches LDS;
+// Wave w owns transform positions (a, b) = (w/2, 2(w%2)) and (w/2, 2(w%2)+1) for all 64
+// tiles; the pair shares its B^T row a, so each wave forms three row combinations
+// R[j] = s0*d[i0][j] + s1*d[i1][j] and both V's from them (24 LDS reads + 5 vector
+// add/subs per 16 tiles x 4 channels; the signs are compile-time per wave group).
+// Per 16-channel slab:
+//   * the tile's (rows+2) x (cols+2) halo of X is staged into LDS once through
+//     range-checked buffer loads (out-of-image / out-of-channel elements read as 0,
+//     branch-free), columns de-interleaved (even columns, then odd) so the stride-2
+//     patch reads of 16 neighbouring tiles are unit-stride, conflict-free ds_read_b128s;
 //   * U fragments are pre-arranged on the host in MFMA fragment order, so each wave
 //     streams its 2 x NF fragments with coalesced 1-KiB loads straight into registers,
 //     one slab ahead;
-//   * 2 positions x 4 tile-frags x NF n-frags x 4 k-steps of v_mfma_f32_16x16x4_f32.
+//   * 2 positions x 4 tile-frags x NF n-frags x 4 k-steps of v_mfma_f32_16x16x4_f32,
+//     with the next tile-fragment's LDS reads issued ahead of each MFMA group.
 // After the last slab the accumulators (M) go through LDS one n-fragment at a time for
 // the cross-position output transform, bias (incl. the folded 1x1 bias per valid tap),
 // activation and store.  Small images split the slab range (ksplit, fixed by H, W, C)
@@ -61,8 +64,9 @@ struct WinoArgs {
 
 constexpr int kWThreads = 512;
 constexpr int kWPitch = 24;      // floats per halo pixel slot (16 channels + 8 pad)
-constexpr int kWMaxHalo = 400;   // halo pixel slots per stage
+constexpr int kWMaxHalo = 400;   // halo pixel slots per stage (+1 trash slot)
 constexpr int kWMsPitch = 17;    // M staging: floats per (position, tile) row of 16 n
+constexpr uint32_t kWInvalid = 0xFFFFFFF0u;  // buffer offset that always reads 0
 
 __device__ __forceinline__ float wact(float v, int act, float slope) {
   if (act == IDF_ACT_RELU) return v > 0.0f ? v : 0.0f;
@@ -83,17 +87,77 @@ __device__ __forceinline__ float wbias(const WinoArgs& g, int n, int y, int x) {
   return bsum;
 }
 
-// B^T row a of F(2,3): V[a][.] = s0 * d[i0][.] + s1 * d[i1][.]
-__device__ __forceinline__ void bt_row(int a, int& i0, int& i1, float& s0, float& s1) {
-  i0 = a == 0 ? 0 : 1;
-  i1 = a == 3 ? 3 : 2;
-  s0 = a == 2 ? -1.0f : 1.0f;
-  s1 = (a == 0 || a == 3) ? -1.0f : 1.0f;
+// B^T of F(2,3): row a combines d[I0(a)] (sign S0(a)) and d[I1(a)] (sign S1(a)).
+template <int a> struct BT {
+  static constexpr int i0 = a == 0 ? 0 : 1;
+  static constexpr int i1 = a == 3 ? 3 : 2;
+  static constexpr bool neg0 = a == 2;
+  static constexpr bool neg1 = a == 0 || a == 3;
+};
+
+template <bool NEG0, bool NEG1>
+__device__ __forceinline__ w4 comb(w4 x0, w4 x1) {
+  if (!NEG0 && !NEG1) return x0 + x1;
+  if (!NEG0 && NEG1) return x0 - x1;
+  if (NEG0 && !NEG1) return x1 - x0;
+  return -(x0 + x1);
+}
+
+// Column slot of halo column j (0..3) relative to a tile's even-half base, de-interleaved.
+__device__ __forceinline__ int colslot(int j, int EH) { return (j & 1) ? EH + (j >> 1) : (j >> 1); }
+
+// One slab of MFMAs for a wave whose positions are (A, 2*BP) and (A, 2*BP + 1).
+template <int NF, int A, int BP>
+__device__ __forceinline__ void wino_slab(const float* __restrict__ lds_a, const int (&tbase)[4],
+                                          int HWp, int EH, int lk, const w4 (&u)[2][NF],
+                                          w4 (&acc)[2][4][NF]) {
+  using RA = BT<A>;
+  constexpr int b0 = 2 * BP, b1 = 2 * BP + 1;
+  using C0 = BT<b0>;
+  using C1 = BT<b1>;
+  // the three halo columns the pair needs: {0,1,2} (BP=0) or {1,2,3} (BP=1)
+  constexpr int j0 = BP, j1 = BP + 1, j2 = BP + 2;
+  const int r0 = RA::i0 * HWp, r1 = RA::i1 * HWp;
+  const int cs0 = colslot(j0, EH), cs1 = colslot(j1, EH), cs2 = colslot(j2, EH);
+  const int o00 = (r0 + cs0) * kWPitch + lk, o01 = (r0 + cs1) * kWPitch + lk,
+            o02 = (r0 + cs2) * kWPitch + lk;
+  const int o10 = (r1 + cs0) * kWPitch + lk, o11 = (r1 + cs1) * kWPitch + lk,
+            o12 = (r1 + cs2) * kWPitch + lk;
+  w4 d[6];
+  auto fetch = [&](int i) {
+    const float* P = lds_a + tbase[i] * kWPitch;
+    d[0] = *(const w4*)(P + o00);
+    d[1] = *(const w4*)(P + o01);
+    d[2] = *(const w4*)(P + o02);
+    d[3] = *(const w4*)(P + o10);
+    d[4] = *(const w4*)(P + o11);
+    d[5] = *(const w4*)(P + o12);
+  };
+  fetch(0);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    // rows: R[j] = s0 d[i0][j] + s1 d[i1][j]
+    const w4 R0 = comb<RA::neg0, RA::neg1>(d[0], d[3]);
+    const w4 R1 = comb<RA::neg0, RA::neg1>(d[1], d[4]);
+    const w4 R2 = comb<RA::neg0, RA::neg1>(d[2], d[5]);
+    // columns of position b: its two columns among {j0, j1, j2}
+    auto pick = [&](int j) -> w4 { return j == j0 ? R0 : (j == j1 ? R1 : R2); };
+    const w4 v0 = comb<C0::neg0, C0::neg1>(pick(C0::i0), pick(C0::i1));
+    const w4 v1 = comb<C1::neg0, C1::neg1>(pick(C1::i0), pick(C1::i1));
+    if (i + 1 < 4) fetch(i + 1);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int jn = 0; jn < NF; ++jn) {
+        acc[0][i][jn] = __builtin_amdgcn_mfma_f32_16x16x4f32(v0[t], u[0][jn][t], acc[0][i][jn], 0, 0, 0);
+        acc[1][i][jn] = __builtin_amdgcn_mfma_f32_16x16x4f32(v1[t], u[1][jn][t], acc[1][i][jn], 0, 0, 0);
+      }
+  }
 }
 
 template <int NF>
 __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
-  constexpr int A_STAGE = kWMaxHalo * kWPitch;
+  constexpr int A_STAGE = (kWMaxHalo + 1) * kWPitch;
   constexpr int A_PER_T = (kWMaxHalo * 4 + kWThreads - 1) / kWThreads;
   static_assert(16 * 64 * kWMsPitch <= 2 * A_STAGE, "M staging aliases the halo buffers");
   __shared__ __attribute__((aligned(16))) float lds[2 * A_STAGE];
@@ -114,26 +178,30 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   const int TTH = g.TH >> 1, TTW = g.TW >> 1, TPI = TTH * TTW;  // wino tiles per image
   const int s_lo = (int)((int64_t)ks * g.nslab / g.ksplit);
   const int s_hi = (int)((int64_t)(ks + 1) * g.nslab / g.ksplit);
-  const int nf0 = nt * NF;  // first global n-fragment of this block
+  const int nf0 = nt * NF;
 
-  // ---- halo staging map: pixel (img, hy, hx) -> de-interleaved slot
-  int64_t a_src[A_PER_T];
-  int a_dst[A_PER_T];
+  // ---- halo staging: buffer resource over the block's images; invalid -> reads 0
+  const float* xbase = g.X + (int64_t)b0 * g.H * g.Wd * g.ldx;
+  const int64_t xbytes = ((int64_t)g.B * g.H * g.Wd * g.ldx - (int64_t)b0 * g.H * g.Wd * g.ldx) * 4;
+  const int nrec = (int)(xbytes < (int64_t)kWInvalid ? xbytes : (int64_t)kWInvalid);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)xbase, 0, nrec, 0x00020000);
+  uint32_t a_src[A_PER_T];  // byte offset of the pixel's channel 4q (slab 0), or kWInvalid
+  int a_dst[A_PER_T];       // LDS float offset (trash slot when beyond the halo)
 #pragma unroll
   for (int j = 0; j < A_PER_T; ++j) {
     const int f = tid + kWThreads * j;
     const int hp = f >> 2, q = f & 3;
-    a_src[j] = -1;
-    a_dst[j] = -1;
+    a_src[j] = kWInvalid;
+    a_dst[j] = kWMaxHalo * kWPitch;  // trash slot
     if (hp < NH) {
       const int img = hp / (HH * HWp);
       const int rem = hp - img * HH * HWp;
       const int hy = rem / HWp, hx = rem - hy * HWp;
       const int slot = (img * HH + hy) * HWp + ((hx & 1) ? EH + (hx >> 1) : (hx >> 1));
       a_dst[j] = slot * kWPitch + 4 * q;
-      const int b = b0 + img, y = y0 + hy - 1, x = x0 + hx - 1;
-      if (b < g.B && y >= 0 && y < g.H && x >= 0 && x < g.Wd)
-        a_src[j] = (((int64_t)b * g.H + y) * g.Wd + x) * g.ldx + 4 * q;
+      const int y = y0 + hy - 1, x = x0 + hx - 1;
+      if (b0 + img < g.B && y >= 0 && y < g.H && x >= 0 && x < g.Wd)
+        a_src[j] = (uint32_t)(((((int64_t)img * g.H + y) * g.Wd + x) * g.ldx + 4 * q) * 4);
     }
   }
   w4 ra[A_PER_T];
@@ -141,15 +209,15 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
     const int c0 = slab * 16;
 #pragma unroll
     for (int j = 0; j < A_PER_T; ++j) {
-      const bool ok = a_src[j] >= 0 && c0 + 4 * ((tid + kWThreads * j) & 3) < g.C;
-      ra[j] = ok ? *(const w4*)(g.X + a_src[j] + c0) : w4{0.f, 0.f, 0.f, 0.f};
+      const bool ok = a_src[j] != kWInvalid && c0 + 4 * ((tid + kWThreads * j) & 3) < g.C;
+      const uint32_t off = ok ? a_src[j] + (uint32_t)c0 * 4u : kWInvalid;
+      ra[j] = __builtin_bit_cast(w4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
     }
   };
   auto store_halo = [&](int buf) {
-    float* A = lds + buf * A_STAGE;
+    float* Ab = lds + buf * A_STAGE;
 #pragma unroll
-    for (int j = 0; j < A_PER_T; ++j)
-      if (a_dst[j] >= 0) *(w4*)(A + a_dst[j]) = ra[j];
+    for (int j = 0; j < A_PER_T; ++j) *(w4*)(Ab + a_dst[j]) = ra[j];
   };
   // ---- U fragments (registers, one slab ahead)
   w4 ucur[2][NF], unxt[2][NF];
@@ -177,15 +245,6 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
     if (img >= g.IMGS) img = 0;  // idle rows read valid LDS
     tbase[i] = (img * HH + 2 * ty) * HWp + tx;
   }
-  int pi0[2], pi1[2], pj0[2], pj1[2];
-  float ps0[2], ps1[2], pt0[2], pt1[2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int p = 2 * wave + q;
-    bt_row(p >> 2, pi0[q], pi1[q], ps0[q], ps1[q]);
-    bt_row(p & 3, pj0[q], pj1[q], pt0[q], pt1[q]);
-  }
-  auto col = [&](int j) { return (j & 1) ? EH + (j >> 1) : (j >> 1); };
 
   w4 acc[2][4][NF];
 #pragma unroll
@@ -201,6 +260,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
     store_halo(0);
   }
   __syncthreads();
+  const int wg = wave;  // wave-uniform: selects (a, b-pair)
   for (int s = s_lo; s < s_hi; ++s) {
     const int buf = (s - s_lo) & 1;
     const bool more = s + 1 < s_hi;
@@ -208,27 +268,16 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
       load_halo(s + 1);
       load_u(s + 1, unxt);
     }
-    const float* A = lds + buf * A_STAGE;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int o00 = (pi0[q] * HWp + col(pj0[q])) * kWPitch + lk;
-      const int o01 = (pi0[q] * HWp + col(pj1[q])) * kWPitch + lk;
-      const int o10 = (pi1[q] * HWp + col(pj0[q])) * kWPitch + lk;
-      const int o11 = (pi1[q] * HWp + col(pj1[q])) * kWPitch + lk;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float* P = A + tbase[i] * kWPitch;
-        const w4 d00 = *(const w4*)(P + o00), d01 = *(const w4*)(P + o01);
-        const w4 d10 = *(const w4*)(P + o10), d11 = *(const w4*)(P + o11);
-        const w4 r0 = d00 * pt0[q] + d01 * pt1[q];
-        const w4 r1 = d10 * pt0[q] + d11 * pt1[q];
-        const w4 v = r0 * ps0[q] + r1 * ps1[q];
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int j = 0; j < NF; ++j)
-            acc[q][i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[t], ucur[q][j][t], acc[q][i][j], 0, 0, 0);
-      }
+    const float* Ab = lds + buf * A_STAGE;
+    switch (wg) {
+      case 0: wino_slab<NF, 0, 0>(Ab, tbase, HWp, EH, lk, ucur, acc); break;
+      case 1: wino_slab<NF, 0, 1>(Ab, tbase, HWp, EH, lk, ucur, acc); break;
+      case 2: wino_slab<NF, 1, 0>(Ab, tbase, HWp, EH, lk, ucur, acc); break;
+      case 3: wino_slab<NF, 1, 1>(Ab, tbase, HWp, EH, lk, ucur, acc); break;
+      case 4: wino_slab<NF, 2, 0>(Ab, tbase, HWp, EH, lk, ucur, acc); break;
+      case 5: wino_slab<NF, 2, 1>(Ab, tbase, HWp, EH, lk, ucur, acc); break;
+      case 6: wino_slab<NF, 3, 0>(Ab, tbase, HWp, EH, lk, ucur, acc); break;
+      default: wino_slab<NF, 3, 1>(Ab, tbase, HWp, EH, lk, ucur, acc); break;
     }
     if (more) {
       store_halo(buf ^ 1);
@@ -371,6 +420,8 @@ extern "C" int idf_conv3x3_wino(void* stream, int32_t B, int32_t H, int32_t W, i
   g.B = B; g.H = H; g.Wd = W;
   WinoPlan pl = wino_plan(H, W, g.nslab);
   if (!pl.ok) return IDF_ERR_UNSUPPORTED;
+  // per-block buffer offsets are 32-bit: the block's images must span < 4 GiB
+  if ((int64_t)pl.IMGS * H * W * ld_x * 4 >= (int64_t)kWInvalid) return IDF_ERR_UNSUPPORTED;
   g.IMGS = pl.IMGS; g.TH = pl.TH; g.TW = pl.TW; g.ksplit = pl.ksplit;
   g.tiles_b = (B + pl.IMGS - 1) / pl.IMGS;
   g.tiles_y = (H + pl.TH - 1) / pl.TH;
