@@ -32,9 +32,18 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "idf_codec_internal.h"
 
 #pragma clang fp contract(off)
+
+// Timing-only ablations for tools/native/wino_ablate (never set in the library build):
+// bit 0 skips the per-slab DMA, bit 1 skips the halo LDS reads, bit 2 skips the MFMAs,
+// bit 3 skips the input transform, bit 4 the in-loop barrier, bit 5 the U loads.
+#ifndef IDF_WINO_ABLATE
+#define IDF_WINO_ABLATE 0
+#endif
 
 namespace idf {
 
@@ -63,8 +72,8 @@ struct WinoArgs {
 };
 
 constexpr int kWThreads = 512;
-constexpr int kWPitch = 24;      // floats per halo pixel slot (16 channels + 8 pad)
-constexpr int kWMaxHalo = 400;   // halo pixel slots per stage (+1 trash slot)
+constexpr int kWMaxHalo = 400;   // halo pixel slots used per stage
+constexpr int kWSlots = 448;     // slots per channel quad of a stage (kWMaxHalo rounded to 64)
 constexpr int kWMsPitch = 17;    // M staging: floats per (position, tile) row of 16 n
 constexpr uint32_t kWInvalid = 0xFFFFFFF0u;  // buffer offset that always reads 0
 
@@ -106,63 +115,81 @@ __device__ __forceinline__ w4 comb(w4 x0, w4 x1) {
 // Column slot of halo column j (0..3) relative to a tile's even-half base, de-interleaved.
 __device__ __forceinline__ int colslot(int j, int EH) { return (j & 1) ? EH + (j >> 1) : (j >> 1); }
 
-// One slab of MFMAs for a wave whose positions are (A, 2*BP) and (A, 2*BP + 1).
+// The work of a wave whose positions are (A, 2*BP) and (A, 2*BP + 1): per tile-fragment i
+// (16 tiles) six halo reads, the shared B^T row combination and 2 x NF x 4 MFMAs.
+// xq: this lane's channel quad of a stage's halo image ([4 quads][kWSlots][4 floats]).
 template <int NF, int A, int BP>
-__device__ __forceinline__ void wino_slab(const float* __restrict__ lds_a, const int (&tbase)[4],
-                                          int HWp, int EH, int lk, const w4 (&u)[2][NF],
-                                          w4 (&acc)[2][4][NF]) {
+struct WinoRole {
   using RA = BT<A>;
-  constexpr int b0 = 2 * BP, b1 = 2 * BP + 1;
-  using C0 = BT<b0>;
-  using C1 = BT<b1>;
+  using C0 = BT<2 * BP>;
+  using C1 = BT<2 * BP + 1>;
   // the three halo columns the pair needs: {0,1,2} (BP=0) or {1,2,3} (BP=1)
-  constexpr int j0 = BP, j1 = BP + 1, j2 = BP + 2;
-  const int r0 = RA::i0 * HWp, r1 = RA::i1 * HWp;
-  const int cs0 = colslot(j0, EH), cs1 = colslot(j1, EH), cs2 = colslot(j2, EH);
-  const int o00 = (r0 + cs0) * kWPitch + lk, o01 = (r0 + cs1) * kWPitch + lk,
-            o02 = (r0 + cs2) * kWPitch + lk;
-  const int o10 = (r1 + cs0) * kWPitch + lk, o11 = (r1 + cs1) * kWPitch + lk,
-            o12 = (r1 + cs2) * kWPitch + lk;
-  w4 d[6];
-  auto fetch = [&](int i) {
-    const float* P = lds_a + tbase[i] * kWPitch;
-    d[0] = *(const w4*)(P + o00);
-    d[1] = *(const w4*)(P + o01);
-    d[2] = *(const w4*)(P + o02);
-    d[3] = *(const w4*)(P + o10);
-    d[4] = *(const w4*)(P + o11);
-    d[5] = *(const w4*)(P + o12);
-  };
-  fetch(0);
+  static constexpr int j0 = BP, j1 = BP + 1, j2 = BP + 2;
+  int o[6];
+
+  __device__ __forceinline__ WinoRole(int HWp, int EH) {
+    const int r0 = RA::i0 * HWp, r1 = RA::i1 * HWp;
+    const int cs0 = colslot(j0, EH), cs1 = colslot(j1, EH), cs2 = colslot(j2, EH);
+    o[0] = (r0 + cs0) * 4; o[1] = (r0 + cs1) * 4; o[2] = (r0 + cs2) * 4;
+    o[3] = (r1 + cs0) * 4; o[4] = (r1 + cs1) * 4; o[5] = (r1 + cs2) * 4;
+  }
+
+  __device__ __forceinline__ void fetch(const float* xq, int tb, w4 (&dd)[6]) const {
+    if (IDF_WINO_ABLATE & 2) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+      for (int e = 0; e < 6; ++e) dd[e] = w4{(float)e, 1.f, 2.f, (float)tb};
+      return;
+    }
+    const float* P = xq + tb * 4;
+#pragma unroll
+    for (int e = 0; e < 6; ++e) dd[e] = *(const w4*)(P + o[e]);
+  }
+
+  __device__ __forceinline__ void transform(const w4 (&dc)[6], w4& v0, w4& v1) const {
+    if (IDF_WINO_ABLATE & 8) {
+      v0 = dc[0];
+      v1 = dc[5];
+      return;
+    }
     // rows: R[j] = s0 d[i0][j] + s1 d[i1][j]
-    const w4 R0 = comb<RA::neg0, RA::neg1>(d[0], d[3]);
-    const w4 R1 = comb<RA::neg0, RA::neg1>(d[1], d[4]);
-    const w4 R2 = comb<RA::neg0, RA::neg1>(d[2], d[5]);
+    const w4 R0 = comb<RA::neg0, RA::neg1>(dc[0], dc[3]);
+    const w4 R1 = comb<RA::neg0, RA::neg1>(dc[1], dc[4]);
+    const w4 R2 = comb<RA::neg0, RA::neg1>(dc[2], dc[5]);
     // columns of position b: its two columns among {j0, j1, j2}
     auto pick = [&](int j) -> w4 { return j == j0 ? R0 : (j == j1 ? R1 : R2); };
-    const w4 v0 = comb<C0::neg0, C0::neg1>(pick(C0::i0), pick(C0::i1));
-    const w4 v1 = comb<C1::neg0, C1::neg1>(pick(C1::i0), pick(C1::i1));
-    if (i + 1 < 4) fetch(i + 1);
+    v0 = comb<C0::neg0, C0::neg1>(pick(C0::i0), pick(C0::i1));
+    v1 = comb<C1::neg0, C1::neg1>(pick(C1::i0), pick(C1::i1));
+  }
+
+  __device__ __forceinline__ static void mfma(const w4& v0, const w4& v1, const w4 (&u)[2][NF],
+                                              w4 (&acc)[NF * 2]) {
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int jn = 0; jn < NF; ++jn) {
-        acc[0][i][jn] = __builtin_amdgcn_mfma_f32_16x16x4f32(v0[t], u[0][jn][t], acc[0][i][jn], 0, 0, 0);
-        acc[1][i][jn] = __builtin_amdgcn_mfma_f32_16x16x4f32(v1[t], u[1][jn][t], acc[1][i][jn], 0, 0, 0);
+        if (IDF_WINO_ABLATE & 4) {
+          acc[jn][t] += v0[t] * u[0][jn][t];
+          acc[NF + jn][t] += v1[t] * u[1][jn][t];
+          continue;
+        }
+        acc[jn] = __builtin_amdgcn_mfma_f32_16x16x4f32(v0[t], u[0][jn][t], acc[jn], 0, 0, 0);
+        acc[NF + jn] = __builtin_amdgcn_mfma_f32_16x16x4f32(v1[t], u[1][jn][t], acc[NF + jn], 0, 0, 0);
       }
   }
-}
+};
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 template <int NF>
 __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
-  constexpr int A_STAGE = (kWMaxHalo + 1) * kWPitch;
-  constexpr int A_PER_T = (kWMaxHalo * 4 + kWThreads - 1) / kWThreads;
-  static_assert(16 * 64 * kWMsPitch <= 2 * A_STAGE, "M staging aliases the halo buffers");
-  __shared__ __attribute__((aligned(16))) float lds[2 * A_STAGE];
+  // one stage = the slab's halo image [4 quads][kWSlots][4 floats]
+  constexpr int STAGE = 4 * kWSlots * 4;
+  constexpr int XI_PER_W = (4 * kWSlots / 64 + 7) / 8;  // halo DMA instructions per wave
+  constexpr int MS = 16 * 64 * kWMsPitch;  // output-transform staging, aliases the stages
+  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE > MS ? 2 * STAGE : MS];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   int bid = blockIdx.x;
   const int ks = bid % g.ksplit;
   bid /= g.ksplit;
@@ -173,68 +200,66 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   const int ty_ = bid % g.tiles_y;
   const int tb = bid / g.tiles_y;
   const int b0 = tb * g.IMGS, y0 = ty_ * g.TH, x0 = tx_ * g.TW;
-  const int HWp = g.TW + 2, HH = g.TH + 2, EH = (HWp + 1) >> 1;
+  const int HWp = g.TW + 2, HH = g.TH + 2, EH = HWp >> 1;  // TW even: HWp even
   const int NH = g.IMGS * HH * HWp;
+  const int nxi = 4 * ((NH + 63) >> 6);  // halo DMA wave-instructions per slab
   const int TTH = g.TH >> 1, TTW = g.TW >> 1, TPI = TTH * TTW;  // wino tiles per image
   const int s_lo = (int)((int64_t)ks * g.nslab / g.ksplit);
   const int s_hi = (int)((int64_t)(ks + 1) * g.nslab / g.ksplit);
   const int nf0 = nt * NF;
 
-  // ---- halo staging: buffer resource over the block's images; invalid -> reads 0
+  // ---- halo DMA: buffer resource over the block's images; out-of-range offsets read 0.
+  // Instruction f = q * nblk + k stages slots [64k, 64k + 64) of channel quad q.
   const float* xbase = g.X + (int64_t)b0 * g.H * g.Wd * g.ldx;
   const int64_t xbytes = ((int64_t)g.B * g.H * g.Wd * g.ldx - (int64_t)b0 * g.H * g.Wd * g.ldx) * 4;
   const int nrec = (int)(xbytes < (int64_t)kWInvalid ? xbytes : (int64_t)kWInvalid);
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)xbase, 0, nrec, 0x00020000);
-  uint32_t a_src[A_PER_T];  // byte offset of the pixel's channel 4q (slab 0), or kWInvalid
-  int a_dst[A_PER_T];       // LDS float offset (trash slot when beyond the halo)
+  const int nblk = nxi >> 2;
+  uint32_t x_src[XI_PER_W];  // byte offset of this lane's slot pixel, channel 4q of slab 0
 #pragma unroll
-  for (int j = 0; j < A_PER_T; ++j) {
-    const int f = tid + kWThreads * j;
-    const int hp = f >> 2, q = f & 3;
-    a_src[j] = kWInvalid;
-    a_dst[j] = kWMaxHalo * kWPitch;  // trash slot
-    if (hp < NH) {
-      const int img = hp / (HH * HWp);
-      const int rem = hp - img * HH * HWp;
-      const int hy = rem / HWp, hx = rem - hy * HWp;
-      const int slot = (img * HH + hy) * HWp + ((hx & 1) ? EH + (hx >> 1) : (hx >> 1));
-      a_dst[j] = slot * kWPitch + 4 * q;
-      const int y = y0 + hy - 1, x = x0 + hx - 1;
-      if (b0 + img < g.B && y >= 0 && y < g.H && x >= 0 && x < g.Wd)
-        a_src[j] = (uint32_t)(((((int64_t)img * g.H + y) * g.Wd + x) * g.ldx + 4 * q) * 4);
+  for (int m = 0; m < XI_PER_W; ++m) {
+    const int f = wave + 8 * m;
+    x_src[m] = kWInvalid;
+    if (f < nxi) {
+      const int q = f / nblk, slot = (f - q * nblk) * 64 + lane;
+      if (slot < NH) {
+        const int img = slot / (HH * HWp);
+        const int rem = slot - img * HH * HWp;
+        const int hy = rem / HWp, cs = rem - hy * HWp;
+        const int hx = cs < EH ? 2 * cs : 2 * (cs - EH) + 1;
+        const int y = y0 + hy - 1, x = x0 + hx - 1;
+        if (b0 + img < g.B && y >= 0 && y < g.H && x >= 0 && x < g.Wd)
+          x_src[m] = (uint32_t)(((((int64_t)img * g.H + y) * g.Wd + x) * g.ldx + 4 * q) * 4);
+      }
     }
   }
-  w4 ra[A_PER_T];
-  auto load_halo = [&](int slab) {
+  auto issue = [&](int slab, int buf) {
+    float* St = lds + buf * STAGE;
     const int c0 = slab * 16;
 #pragma unroll
-    for (int j = 0; j < A_PER_T; ++j) {
-      const bool ok = a_src[j] != kWInvalid && c0 + 4 * ((tid + kWThreads * j) & 3) < g.C;
-      const uint32_t off = ok ? a_src[j] + (uint32_t)c0 * 4u : kWInvalid;
-      ra[j] = __builtin_bit_cast(w4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+    for (int m = 0; m < XI_PER_W; ++m) {
+      const int f = wave + 8 * m;
+      if (f < nxi) {
+        const int q = f / nblk, k = f - q * nblk;
+        const bool ok = x_src[m] != kWInvalid && c0 + 4 * q < g.C;
+        const uint32_t off = ok ? x_src[m] + (uint32_t)c0 * 4u : kWInvalid;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_ptr_t)(St + (q * kWSlots + 64 * k) * 4),
+                                                 16, off, 0, 0, 0);
+      }
     }
   };
-  auto store_halo = [&](int buf) {
-    float* Ab = lds + buf * A_STAGE;
-#pragma unroll
-    for (int j = 0; j < A_PER_T; ++j) *(w4*)(Ab + a_dst[j]) = ra[j];
-  };
-  // ---- U fragments (registers, one slab ahead)
-  w4 ucur[2][NF], unxt[2][NF];
+  // this wave's two positions of U, NF fragments each, straight into registers
   auto load_u = [&](int slab, w4 (&u)[2][NF]) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const int p = 2 * wave + q;
+      const float* ub = g.U + (((int64_t)(2 * wave + q) * g.nslab + slab) * g.nft + nf0) * 256;
 #pragma unroll
-      for (int j = 0; j < NF; ++j) {
-        const int64_t o = ((((int64_t)p * g.nslab + slab) * g.nft + nf0 + j) * 64 + lane) * 4;
-        u[q][j] = *(const w4*)(g.U + o);
-      }
+      for (int j = 0; j < NF; ++j) u[q][j] = *(const w4*)(ub + j * 256 + lane * 4);
     }
   };
 
   // ---- per-lane tile bases (slot of the patch's top-left, even-column half)
-  const int lr = lane & 15, lk = 4 * (lane >> 4);
+  const int lr = lane & 15, lq = lane >> 4;
   int tbase[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -246,47 +271,74 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
     tbase[i] = (img * HH + 2 * ty) * HWp + tx;
   }
 
-  w4 acc[2][4][NF];
+  w4 acc[4][2 * NF];  // [tile fragment][position q * NF + n-fragment]
 #pragma unroll
-  for (int q = 0; q < 2; ++q)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < NF; ++j) acc[q][i][j] = w4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 2 * NF; ++j) acc[i][j] = w4{0.f, 0.f, 0.f, 0.f};
 
-  if (s_lo < s_hi) {
-    load_halo(s_lo);
-    load_u(s_lo, ucur);
-    store_halo(0);
-  }
-  __syncthreads();
-  const int wg = wave;  // wave-uniform: selects (a, b-pair)
-  for (int s = s_lo; s < s_hi; ++s) {
-    const int buf = (s - s_lo) & 1;
-    const bool more = s + 1 < s_hi;
-    if (more) {
-      load_halo(s + 1);
-      load_u(s + 1, unxt);
+  // The slab loop is instantiated per wave role (A, BP) so that each role's loop-invariant
+  // LDS addresses are the only ones live in its loop.  Software pipeline per slab s
+  // (tile-fragment groups g0..g3, each = transform + MFMAs, with the next group's halo
+  // reads in flight under it):
+  //   g0: issue the DMA of slab s+1's halo into the other stage, and slab s+1's U loads
+  //   g2: after its MFMAs, barrier -- slab s+1's halo has landed and every wave has
+  //       finished reading stage s (its last reads, for g3, were issued in g2)
+  //   g3: its reads are already in registers; it prefetches g0 of slab s+1
+  // so no wave starts a slab waiting on LDS, and the barrier sits where every wave still
+  // has a full MFMA group queued behind it.
+  auto run = [&](auto a_tag, auto bp_tag) {
+    constexpr int A = decltype(a_tag)::value, BP = decltype(bp_tag)::value;
+    const WinoRole<NF, A, BP> role(HWp, EH);
+    w4 ucur[2][NF], unxt[2][NF];
+    w4 d[2][6];
+    if (s_lo < s_hi) {
+      issue(s_lo, 0);
+      load_u(s_lo, ucur);
     }
-    const float* Ab = lds + buf * A_STAGE;
-    switch (wg) {
-      case 0: wino_slab<NF, 0, 0>(Ab, tbase, HWp, EH, lk, ucur, acc); break;
-      case 1: wino_slab<NF, 0, 1>(Ab, tbase, HWp, EH, lk, ucur, acc); break;
-      case 2: wino_slab<NF, 1, 0>(Ab, tbase, HWp, EH, lk, ucur, acc); break;
-      case 3: wino_slab<NF, 1, 1>(Ab, tbase, HWp, EH, lk, ucur, acc); break;
-      case 4: wino_slab<NF, 2, 0>(Ab, tbase, HWp, EH, lk, ucur, acc); break;
-      case 5: wino_slab<NF, 2, 1>(Ab, tbase, HWp, EH, lk, ucur, acc); break;
-      case 6: wino_slab<NF, 3, 0>(Ab, tbase, HWp, EH, lk, ucur, acc); break;
-      default: wino_slab<NF, 3, 1>(Ab, tbase, HWp, EH, lk, ucur, acc); break;
-    }
-    if (more) {
-      store_halo(buf ^ 1);
+    __syncthreads();  // waits for the DMA (vmcnt) before the barrier
+    if (s_lo < s_hi) role.fetch(lds + lq * kWSlots * 4, tbase[0], d[0]);
+    for (int s = s_lo; s < s_hi; ++s) {
+      const int buf = (s - s_lo) & 1;
+      const bool more = s + 1 < s_hi;
+      const float* xq = lds + buf * STAGE + lq * kWSlots * 4;
+      const float* xn = lds + (buf ^ 1) * STAGE + lq * kWSlots * 4;
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
+      for (int i = 0; i < 4; ++i) {
+        w4 v0, v1;
+        role.transform(d[i & 1], v0, v1);
+        if (i < 3) role.fetch(xq, tbase[i + 1], d[(i + 1) & 1]);
+        else if (more) role.fetch(xn, tbase[0], d[0]);
+        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMAs
+        role.mfma(v0, v1, ucur, acc[i]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (i == 0 && more) {
+          if (!(IDF_WINO_ABLATE & 1)) issue(s + 1, buf ^ 1);
+          if (!(IDF_WINO_ABLATE & 32)) load_u(s + 1, unxt);
+        }
+        if (i == 2 && !(IDF_WINO_ABLATE & 16)) __syncthreads();
+      }
+      if (more) {
 #pragma unroll
-        for (int j = 0; j < NF; ++j) ucur[q][j] = unxt[q][j];
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int j = 0; j < NF; ++j) ucur[q][j] = unxt[q][j];
+      }
     }
-    __syncthreads();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  switch (wave) {
+    case 0: run(I0{}, I0{}); break;
+    case 1: run(I0{}, I1{}); break;
+    case 2: run(I1{}, I0{}); break;
+    case 3: run(I1{}, I1{}); break;
+    case 4: run(I2{}, I0{}); break;
+    case 5: run(I2{}, I1{}); break;
+    case 6: run(I3{}, I0{}); break;
+    default: run(I3{}, I1{}); break;
   }
 
   // ---- output transform, one n-fragment at a time through LDS
@@ -301,7 +353,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int t = 16 * i + (lane >> 4) * 4 + r;
-          Ms[(p * 64 + t) * kWMsPitch + lr] = acc[q][i][j][r];
+          Ms[(p * 64 + t) * kWMsPitch + lr] = acc[i][q * NF + j][r];
         }
     }
     __syncthreads();

@@ -1,6 +1,7 @@
 """Kernel microbenchmark of the folded 3x3 conv at the imagenet64 shapes (B=256): the LDS
 halo-tiled kernel (idf_conv3x3_halo) and the implicit-GEMM kernel (idf_conv3x3_fold_f32),
-per level and layer width.  Prints achieved TFLOP/s (unpadded FLOPs)."""
+per level and layer width.  Prints achieved TFLOP/s (unpadded FLOPs).
+Env filters: KB_ONLY=wino,halo,gemm  KB_LEVELS=0,1,2  KB_LAYERS=0,3,6,9,11  KB_REPS=10."""
 import os
 import sys
 
@@ -32,12 +33,18 @@ def main():
     dev = torch.device("cuda")
     s = _lib.stream_ptr()
     g_pad, g_alloc, g_real = 44, 48, 43
-    tot = {"wino": [0.0, 0.0], "halo": [0.0, 0.0], "gemm": [0.0, 0.0]}
+    only = os.environ.get("KB_ONLY", "wino,halo,gemm").split(",")
+    layers = [int(v) for v in os.environ.get("KB_LAYERS", "0,3,6,9,11").split(",")]
+    levels = [int(v) for v in os.environ.get("KB_LEVELS", "0,1,2").split(",")]
+    reps = int(os.environ.get("KB_REPS", "10"))
+    tot = {k: [0.0, 0.0] for k in only}
     import numpy as np
     from idfcodec.packing import wino_weights
     for lvl, (hw, a) in enumerate(((32, 9), (16, 18), (8, 36))):
+        if lvl not in levels:
+            continue
         P = B * hw * hw
-        for layer in (0, 3, 6, 9, 11):
+        for layer in layers:
             c_pad = round_up(a, 4) + layer * g_pad
             c_real = a + layer * 512 // 12
             ld = round_up(c_pad + g_pad, 16)
@@ -71,13 +78,16 @@ def main():
                                                  ptr(feat) + c_pad * 4, ld, 0, 0.0), "gemm")
             line = f"L{lvl} hw={hw:2d} c={c_pad:4d} P={P:7d}"
             for name, fn in (("wino", wino), ("halo", halo), ("gemm", gemm)):
-                ms = time_it(fn)
+                if name not in only:
+                    continue
+                ms = time_it(fn, reps)
                 tot[name][0] += ms
                 tot[name][1] += fl
                 line += f"  {name} {ms*1e3:8.1f} us {fl/ms/1e9:6.1f} TF/s"
             print(line, flush=True)
     for k, (ms, fl) in tot.items():
-        print(f"{k}: sampled total {ms:.2f} ms  {fl/ms/1e9:.1f} TF/s")
+        if ms > 0:
+            print(f"{k}: sampled total {ms:.2f} ms  {fl/ms/1e9:.1f} TF/s")
 
 
 if __name__ == "__main__":

@@ -1,0 +1,50 @@
+// Timing-only ablation harness for the Winograd conv kernel: built once per
+// IDF_WINO_ABLATE value (tools/native/Makefile), times the imagenet64 level-0 and level-2
+// widest layers on random data.  Outputs are meaningless for ablate != 0.
+#include "../../finalproject-losslessimagecompression_amd/csrc/conv3_wino.hip"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <vector>
+
+static float* dev_random(size_t n) {
+  std::vector<float> h(n);
+  for (size_t i = 0; i < n; ++i) h[i] = (float)rand() / RAND_MAX - 0.5f;
+  float* d;
+  if (hipMalloc(&d, n * 4) != hipSuccess) abort();
+  if (hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess) abort();
+  return d;
+}
+
+int main() {
+  struct Case { int B, hw, c; } cases[] = {{256, 32, 496}, {256, 16, 504}, {256, 8, 520}};
+  const int N = 44, n_alloc = 48;
+  for (auto& cs : cases) {
+    const int P = cs.B * cs.hw * cs.hw, ld = (cs.c + N + 15) / 16 * 16, nslab = (cs.c + 15) / 16;
+    float* X = dev_random((size_t)P * ld);
+    float* U = dev_random((size_t)16 * nslab * (n_alloc / 16) * 256);
+    float* b = dev_random(n_alloc * 10);
+    const int64_t wsn = idf_conv3x3_wino_workspace(cs.B, cs.hw, cs.hw, cs.c, N);
+    float* ws = wsn ? dev_random(wsn) : nullptr;
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    float best = 1e9f;
+    for (int rep = 0; rep < 6; ++rep) {
+      (void)hipEventRecord(e0, 0);
+      int rc = idf_conv3x3_wino(nullptr, cs.B, cs.hw, cs.hw, cs.c, X, ld, U, n_alloc / 16, b, b + n_alloc,
+                                n_alloc, b + 8 * n_alloc, N, X + cs.c, ld, 1, 0.f, ws, wsn);
+      (void)hipEventRecord(e1, 0);
+      (void)hipEventSynchronize(e1);
+      if (rc) { printf("rc=%d\n", rc); return 1; }
+      float ms;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      if (rep && ms < best) best = ms;
+    }
+    const double mfma = 2.0 * cs.B * (cs.hw / 2) * (cs.hw / 2) * 16 * (nslab * 16.0) * n_alloc;
+    printf("ablate=%d hw=%d c=%d: %.1f us  executed-MFMA %.1f TF/s\n", IDF_WINO_ABLATE, cs.hw, cs.c,
+           best * 1e3, mfma / best / 1e9);
+    (void)hipFree(X); (void)hipFree(U); (void)hipFree(b); if (ws) (void)hipFree(ws);
+  }
+  return 0;
+}
