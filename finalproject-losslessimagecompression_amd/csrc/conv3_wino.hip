@@ -44,6 +44,11 @@
 #ifndef IDF_WINO_ABLATE
 #define IDF_WINO_ABLATE 0
 #endif
+// Where the next slab's loads are issued: 0 = halo DMA + U after group 0's MFMAs,
+// 1 = halo after group 0, U after group 1, 2 = halo pieces between group 1's k-steps.
+#ifndef IDF_WINO_SCHED
+#define IDF_WINO_SCHED 2
+#endif
 
 namespace idf {
 
@@ -161,10 +166,12 @@ struct WinoRole {
     v1 = comb<C1::neg0, C1::neg1>(pick(C1::i0), pick(C1::i1));
   }
 
+  template <typename Hook>
   __device__ __forceinline__ static void mfma(const w4& v0, const w4& v1, const w4 (&u)[2][NF],
-                                              w4 (&acc)[NF * 2]) {
+                                              w4 (&acc)[NF * 2], Hook&& hook) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 4; ++t) {
+      if (t) hook(t - 1);  // between k-steps: room for a load's issue under queued MFMAs
 #pragma unroll
       for (int jn = 0; jn < NF; ++jn) {
         if (IDF_WINO_ABLATE & 4) {
@@ -175,6 +182,7 @@ struct WinoRole {
         acc[jn] = __builtin_amdgcn_mfma_f32_16x16x4f32(v0[t], u[0][jn][t], acc[jn], 0, 0, 0);
         acc[NF + jn] = __builtin_amdgcn_mfma_f32_16x16x4f32(v1[t], u[1][jn][t], acc[NF + jn], 0, 0, 0);
       }
+    }
   }
 };
 
@@ -233,11 +241,10 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
       }
     }
   }
-  auto issue = [&](int slab, int buf) {
+  auto issue_piece = [&](int slab, int buf, int m) {
     float* St = lds + buf * STAGE;
     const int c0 = slab * 16;
-#pragma unroll
-    for (int m = 0; m < XI_PER_W; ++m) {
+    {
       const int f = wave + 8 * m;
       if (f < nxi) {
         const int q = f / nblk, k = f - q * nblk;
@@ -247,6 +254,10 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
                                                  16, off, 0, 0, 0);
       }
     }
+  };
+  auto issue = [&](int slab, int buf) {
+#pragma unroll
+    for (int m = 0; m < XI_PER_W; ++m) issue_piece(slab, buf, m);
   };
   // this wave's two positions of U, NF fragments each, straight into registers
   auto load_u = [&](int slab, w4 (&u)[2][NF]) {
@@ -310,11 +321,30 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
         if (i < 3) role.fetch(xq, tbase[i + 1], d[(i + 1) & 1]);
         else if (more) role.fetch(xn, tbase[0], d[0]);
         __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMAs
-        role.mfma(v0, v1, ucur, acc[i]);
+        if (IDF_WINO_SCHED == 2 && i == 1) {
+          // halo pieces between group 1's k-steps, U loads after it
+          role.mfma(v0, v1, ucur, acc[i], [&](int t) {
+            if (more && !(IDF_WINO_ABLATE & 1) && t < XI_PER_W) issue_piece(s + 1, buf ^ 1, t);
+          });
+        } else {
+          role.mfma(v0, v1, ucur, acc[i], [](int) {});
+        }
         __builtin_amdgcn_sched_barrier(0);
-        if (i == 0 && more) {
-          if (!(IDF_WINO_ABLATE & 1)) issue(s + 1, buf ^ 1);
-          if (!(IDF_WINO_ABLATE & 32)) load_u(s + 1, unxt);
+        if (more) {
+          if (IDF_WINO_SCHED == 0 && i == 0) {
+            if (!(IDF_WINO_ABLATE & 1)) issue(s + 1, buf ^ 1);
+            if (!(IDF_WINO_ABLATE & 32)) load_u(s + 1, unxt);
+          }
+          if (IDF_WINO_SCHED == 1) {
+            if (i == 0 && !(IDF_WINO_ABLATE & 1)) issue(s + 1, buf ^ 1);
+            if (i == 1 && !(IDF_WINO_ABLATE & 32)) load_u(s + 1, unxt);
+          }
+          if (IDF_WINO_SCHED == 2 && i == 1) {
+#pragma unroll
+            for (int m = 3; m < XI_PER_W; ++m)
+              if (!(IDF_WINO_ABLATE & 1)) issue_piece(s + 1, buf ^ 1, m);
+            if (!(IDF_WINO_ABLATE & 32)) load_u(s + 1, unxt);
+          }
         }
         if (i == 2 && !(IDF_WINO_ABLATE & 16)) __syncthreads();
       }

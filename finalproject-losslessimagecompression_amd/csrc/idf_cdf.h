@@ -79,7 +79,7 @@ IDF_HD double fma_d(double a, double b, double c) {
 
 // glibc 2.35 sysdeps/ieee754/flt-32/e_expf.c (EXP2F_TABLE_BITS = 5, poly order 3),
 // as compiled with FMA contraction (x86-64 ifunc __expf_fma).
-IDF_HD float expf_glibc(float x) {
+IDF_HD float expf_glibc(float x, const uint64_t* tab = kExp2fTab) {
   const double InvLn2N = 0x1.71547652b82fep+0 * 32;
   const double SHIFT = 0x1.8p+52;
   const double C0 = 0x1.c6af84b912394p-5 / (32.0 * 32.0 * 32.0);
@@ -98,7 +98,7 @@ IDF_HD float expf_glibc(float x) {
   uint64_t ki = d2u(kd);
   kd -= SHIFT;
   double r = fma_d(InvLn2N, xd, -kd);
-  uint64_t t = kExp2fTab[ki % 32];
+  uint64_t t = tab[ki % 32];
   t += ki << 47;
   double s = u2d(t);
   double z = fma_d(C0, r, C1);
@@ -126,12 +126,15 @@ IDF_HD float round_f(float v) {
 
 // rans.pyx:31-35 (rans.cpp:1418-1449). Returns part1 + part2.
 // Caller guarantees scale != 0 (the reference raises ZeroDivisionError).
-IDF_HD int rans_cdf(float x, float mean, float scale, float lower) {
+// tab: the 2^(j/32) table; device hot loops pass a copy in LDS (kExp2fTab itself is a
+// constant-memory load per lookup, a long latency inside a serial decode chain).
+IDF_HD int rans_cdf(float x, float mean, float scale, float lower,
+                    const uint64_t* tab = kExp2fTab) {
   float d = x - lower;                                        // f32 subtraction
   int part2 = (int)round_d((double)d * 256.0) + 1;            // libm round (double)
   double t = ((double)x + 0.001953125) - (double)mean;       // (x + 0.5/256) - mean in f64
   float u = (float)(t / (double)scale);                       // logistic(float) argument
-  double l = 1.0 / (1.0 + (double)expf_glibc(-u));           // logistic, rans.pyx:26
+  double l = 1.0 / (1.0 + (double)expf_glibc(-u, tab));      // logistic, rans.pyx:26
   float p = (float)(l * 16775168.0);                          // * (M - 2048) then PyFloat->float
   int part1 = (int)round_f(p);                                // (int)round(float) -> roundf
   return part1 + part2;

@@ -8,18 +8,22 @@
 // Kernels
 //   rans_cdf_freq   : pass 1 of encode (rans.pyx:50-56), one thread per symbol,
 //                     fully parallel, HBM-bound (12 B in, 8 B out per symbol).
+//   rans_encode_prep: the streamed encoder's pass 1: (start, freq), the window
+//                     flag and 1/freq per symbol, fully parallel.
 //   rans_encode     : pass 2 (rans.pyx:61-66), one lane per stream; the serial
-//                     state chain with an exact 64/24-bit division done by a
-//                     double-precision reciprocal estimate plus integer correction.
+//                     state chain with an exact 64/24-bit division done by the
+//                     precomputed double reciprocal plus integer correction, its
+//                     symbol records loaded 8 ahead of the chain.
 //   rans_decode     : rans.pyx:69-110, ONE WAVE per stream.  The reference's
 //                     11-12 step binary search over the 2048-bin window is
-//                     replaced by a two-round 64-ary search (round 1: 64 lanes
-//                     probe the last bin of each 32-bin block; round 2: 33 lanes
-//                     probe the chosen block and its left neighbour).  The CDF is
-//                     strictly increasing in s for scale > 0 (part2 steps by 1,
-//                     part1 is monotone: glibc expf verified monotone on every
-//                     float), so both searches return the same s; scale <= 0 or
-//                     NaN falls back to the reference's serial binary search.
+//                     replaced by ONE round of 64 exact CDF probes placed by two
+//                     cheap float rounds (exact_window), with a two-round exact
+//                     64-ary search (exact_search) whenever the window does not
+//                     provably bracket the answer.  The CDF is strictly increasing
+//                     in s for scale > 0 (part2 steps by 1, part1 is monotone:
+//                     glibc expf verified monotone on every float), so every
+//                     search returns the reference's s; scale <= 0 or NaN falls
+//                     back to the reference's serial binary search.
 //   gather_words    : compacts per-stream word runs into one contiguous buffer.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -28,6 +32,22 @@
 #include "idf_codec_internal.h"
 
 #pragma clang fp contract(off)
+
+// Timing-only decode variants for tools/native/rans_bench (never set in the library build):
+// 1 = always the two-round exact search, 2 = exact window without the hoisted divisions,
+// 3 = no search at all (fake symbol), 4 = approximate rounds only, 5 = count fallbacks.
+#ifndef IDF_DECODE_MODE
+#define IDF_DECODE_MODE 0
+#endif
+#if IDF_DECODE_MODE == 5
+__device__ unsigned long long g_decode_fallbacks;
+#endif
+#if IDF_DECODE_MODE == 6
+__device__ unsigned long long g_stamp[256][6];
+#define STAMP(j) do { if (blockIdx.x == 0 && g_sym < 256) g_stamp[g_sym][j] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define STAMP(j) do { } while (0)
+#endif
 
 namespace idf {
 
@@ -63,6 +83,39 @@ __global__ void __launch_bounds__(256) rans_cdf_freq_kernel(int64_t n, const flo
 }
 
 // ---------------------------------------------------------------- pass 2
+// Pass 1 for the streamed encoder: everything per symbol that does not depend on the
+// state chain -- (start, freq), the window flag and the divisor's reciprocal -- so the
+// serial pass 2 is a load, a compare, one multiply-correct division and an add.
+struct EncSym {
+  int32_t start, freq, wflag, pad;
+};
+
+__global__ void __launch_bounds__(256) rans_encode_prep_kernel(
+    int64_t n, const float* __restrict__ x, const float* __restrict__ mean,
+    const float* __restrict__ scale, EncSym* __restrict__ sym, double* __restrict__ rcp) {
+  __shared__ uint64_t tab[32];
+  if (threadIdx.x < 32) tab[threadIdx.x] = kExp2fTab[threadIdx.x];
+  __syncthreads();
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float xi = x[i], mi = mean[i], si = scale[i];
+  EncSym e = {0, IDF_FREQ_SCALE_ZERO, 0, 0};
+  double r = 0.0;
+  const int lo = rans_lower_int(mi);
+  if (si != 0.0f) {  // ZeroDivisionError("float division"), rans.cpp:1435-1438
+    float lower = rans_lower_f(lo);  // rans.pyx:51
+    float xm = (float)((double)xi - 1.0 / 256.0);
+    e.start = rans_cdf(xm, mi, si, lower, tab);      // rans.pyx:52
+    e.freq = rans_cdf(xi, mi, si, lower, tab) - e.start;  // rans.pyx:53
+    if (e.freq >= 1 && e.freq <= (1 << 24)) r = 1.0 / (double)(uint32_t)e.freq;
+  }
+  int32_t f = 0;
+  window_check(xi, lo, &f);
+  e.wflag = f;
+  sym[i] = e;
+  rcp[i] = r;
+}
+
 // Exact q = state / f, r = state % f for f in [1, 2^24], state < 2^64 with q < 2^40
 // (guaranteed after renormalisation).  The double estimate is within +-1.
 __device__ __forceinline__ void divmod_u64_u24(uint64_t state, uint32_t f, double rcp, uint64_t& q,
@@ -80,10 +133,13 @@ __device__ __forceinline__ void divmod_u64_u24(uint64_t state, uint32_t f, doubl
   r = (uint64_t)rr;
 }
 
+// Pass 2, one lane per stream (rans.pyx:61-66).  Symbol records are loaded kEncAhead
+// symbols ahead of the state chain so the chain never waits on memory.
+constexpr int kEncAhead = 8;
+
 __global__ void __launch_bounds__(64) rans_encode_kernel(
-    int64_t nstreams, const int64_t* __restrict__ sym_off, const float* __restrict__ x,
-    const float* __restrict__ mean, const int32_t* __restrict__ start,
-    const int32_t* __restrict__ freq, const uint64_t* __restrict__ init_state,
+    int64_t nstreams, const int64_t* __restrict__ sym_off, const EncSym* __restrict__ sym,
+    const double* __restrict__ rcp, const uint64_t* __restrict__ init_state,
     uint64_t* __restrict__ final_state, uint32_t* __restrict__ words, int64_t* __restrict__ nwords,
     int32_t* __restrict__ status) {
   int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -93,32 +149,56 @@ __global__ void __launch_bounds__(64) rans_encode_kernel(
   uint32_t* out = words + b;
   int64_t nw = 0;
   int32_t flag = 0;
-  for (int64_t i = b; i < e; ++i) {
-    int32_t st = start[i];
-    int32_t fr = freq[i];
-    if (fr == IDF_FREQ_SCALE_ZERO && st == 0) {
-      flag |= IDF_STREAM_SCALE_ZERO;
-      break;
+  EncSym cur[kEncAhead], nxt[kEncAhead];
+  double rc_cur[kEncAhead], rc_nxt[kEncAhead];
+  auto load = [&](int64_t i0, EncSym (&sv)[kEncAhead], double (&rv)[kEncAhead]) {
+#pragma unroll
+    for (int u = 0; u < kEncAhead; ++u) {
+      if (i0 + u < e) {
+        sv[u] = sym[i0 + u];
+        rv[u] = rcp[i0 + u];
+      }
     }
-    uint64_t cdf = (uint64_t)(int64_t)st;  // vector<ull>.push_back(int)
-    uint64_t f = (uint64_t)(int64_t)fr;
-    if (state >= (f << 40)) {  // rans.pyx:62-64
-      out[nw++] = (uint32_t)(state & 0xffffffffull);
-      state >>= 32;
+  };
+  load(b, cur, rc_cur);
+  bool stop = false;
+  for (int64_t i0 = b; i0 < e && !stop; i0 += kEncAhead) {
+    if (i0 + kEncAhead < e) load(i0 + kEncAhead, nxt, rc_nxt);
+#pragma unroll
+    for (int u = 0; u < kEncAhead; ++u) {
+      if (i0 + u >= e) break;
+      const int32_t st = cur[u].start, fr = cur[u].freq;
+      if (fr == IDF_FREQ_SCALE_ZERO && st == 0) {
+        flag |= IDF_STREAM_SCALE_ZERO;
+        stop = true;
+        break;
+      }
+      uint64_t cdf = (uint64_t)(int64_t)st;  // vector<ull>.push_back(int)
+      uint64_t f = (uint64_t)(int64_t)fr;
+      if (state >= (f << 40)) {  // rans.pyx:62-64
+        out[nw++] = (uint32_t)(state & 0xffffffffull);
+        state >>= 32;
+      }
+      if (f == 0) {  // ZeroDivisionError, rans.cpp:1825-1834
+        flag |= IDF_STREAM_FREQ_ZERO;
+        stop = true;
+        break;
+      }
+      uint64_t q, r;
+      if (f <= (1ull << 24)) {
+        divmod_u64_u24(state, (uint32_t)f, rc_cur[u], q, r);
+      } else {  // only reachable out of window / corrupted input: exact slow path
+        q = state / f;
+        r = state % f;
+      }
+      state = (q << 24) + r + cdf;  // rans.pyx:65
+      flag |= cur[u].wflag;
     }
-    if (f == 0) {  // ZeroDivisionError, rans.cpp:1825-1834
-      flag |= IDF_STREAM_FREQ_ZERO;
-      break;
+#pragma unroll
+    for (int u = 0; u < kEncAhead; ++u) {
+      cur[u] = nxt[u];
+      rc_cur[u] = rc_nxt[u];
     }
-    uint64_t q, r;
-    if (f <= (1ull << 24)) {
-      divmod_u64_u24(state, (uint32_t)f, 1.0 / (double)(uint32_t)f, q, r);
-    } else {  // only reachable out of window / corrupted input: exact slow path
-      q = state / f;
-      r = state % f;
-    }
-    state = (q << 24) + r + cdf;  // rans.pyx:65
-    window_check(x[i], rans_lower_int(mean[i]), &flag);
   }
   final_state[k] = state;
   nwords[k] = nw;
@@ -131,16 +211,126 @@ __device__ __forceinline__ float sym_x(int s) { return (float)((double)s / 256.0
 // Reference binary search (rans.pyx:96-104) for the non-monotone corner
 // (scale <= 0 or NaN).  Returns s and flags.
 __device__ int ref_binary_search(uint64_t mod, int lower, float mean, float scale, float lf,
-                                 int32_t* flag) {
+                                 int32_t* flag, const uint64_t* tab) {
   int upper = lower + 0x7FF;
   while (lower <= upper) {
     int s = (lower + upper) >> 1;
-    int c = rans_cdf(sym_x(s), mean, scale, lf);
+    int c = rans_cdf(sym_x(s), mean, scale, lf, tab);
     if (c < 0) *flag |= IDF_STREAM_NEG_CDF;
     if ((uint64_t)(int64_t)c > mod) upper = s - 1;
     else lower = s + 1;
   }
   return lower;
+}
+
+// ---- bit-exact CDF with the divisions in their unscaled form.
+// hipcc lowers a f64 division x / y to v_div_scale (x2), v_rcp + two Newton steps on the
+// scaled y, q = x * r, a residual FMA, v_div_fmas and v_div_fixup.  For the operands the
+// coder produces (float inputs widened to double, |quotient| far inside the double
+// range, finite nonzero y) div_scale leaves both operands unchanged (VCC = 0), div_fmas
+// is a plain FMA and div_fixup returns its input, so the same arithmetic without them is
+// bit-identical; the y-only half (the refined reciprocal) is hoisted per symbol.
+__device__ __forceinline__ double rcp_refined(double y) {
+  double r = __builtin_amdgcn_rcp(y);
+  r = __builtin_fma(r, __builtin_fma(-y, r, 1.0), r);
+  return __builtin_fma(r, __builtin_fma(-y, r, 1.0), r);
+}
+__device__ __forceinline__ double div_unscaled(double x, double y, double r) {
+  const double q = x * r;
+  return __builtin_fma(__builtin_fma(-y, q, x), r, q);
+}
+// scale range in which the hoisted division is used (else rans_cdf's own '/')
+__device__ __forceinline__ bool fast_scale_ok(float scale) {
+  return scale >= 0x1p-60f && scale <= 0x1p60f;
+}
+// rans_cdf (idf_cdf.h) with rs = rcp_refined((double)scale), fast_scale_ok(scale).
+__device__ __forceinline__ int rans_cdf_rs(float x, float mean, float scale, float lower,
+                                           const uint64_t* tab, double rs) {
+  float d = x - lower;
+  int part2 = (int)round_d((double)d * 256.0) + 1;
+  double t = ((double)x + 0.001953125) - (double)mean;
+  float u = (float)div_unscaled(t, (double)scale, rs);
+  double y = 1.0 + (double)expf_glibc(-u, tab);
+  double l = __builtin_isinf(y) ? 0.0 : div_unscaled(1.0, y, rcp_refined(y));
+  float p = (float)(l * 16775168.0);
+  int part1 = (int)round_f(p);
+  return part1 + part2;
+}
+
+// Fast float estimate of the CDF (not bit-exact): used only to place the exact probe
+// window.  part2 (= s - lower + 1) is exact; part1's error is a few units of M.
+__device__ __forceinline__ int approx_cdf(int q, int lower, float mean, float rscale) {
+  const float u = ((float)q * (1.0f / 256.0f) + 0.001953125f - mean) * rscale;
+  const float l = __frcp_rn(1.0f + __expf(-u));
+  return (int)rintf(l * 16775168.0f) + (q - lower + 1);
+}
+
+// Exact two-round 64-ary search over the reference window (rans.pyx:96-104 result):
+// round 1: lane L probes the last bin of block L; round 2: 33 lanes probe the chosen
+// block and its left neighbour.
+__device__ __forceinline__ void exact_search(uint64_t mod, int lower, float mi, float si, float lf,
+                                             int lane, int* s_out, int* c_lo, int* c_hi,
+                                             const uint64_t* tab) {
+  int p1 = lower + 32 * lane + 31;
+  int c1 = rans_cdf(sym_x(p1), mi, si, lf, tab);
+  uint64_t m1 = __ballot((uint64_t)(int64_t)c1 > mod);
+  if (m1 == 0) {
+    // no bin in the window has CDF > mod: reference leaves s = lower + 2048
+    int s = lower + 2048;
+    int q = s - 1 + (lane & 1);
+    int cq = rans_cdf(sym_x(q), mi, si, lf, tab);
+    *s_out = s;
+    *c_lo = __shfl(cq, 0);
+    *c_hi = __shfl(cq, 1);
+    return;
+  }
+  int blk = __ffsll((unsigned long long)m1) - 1;
+  int base = lower + 32 * blk - 1;  // probe base-1 .. base+31 (33 points)
+  int q = base + (lane <= 32 ? lane : 32);
+  int cq = rans_cdf(sym_x(q), mi, si, lf, tab);
+  uint64_t m2 = __ballot(lane >= 1 && lane <= 32 && (uint64_t)(int64_t)cq > mod);
+  int kk = __ffsll((unsigned long long)m2) - 1;  // >= 1
+  *s_out = base + kk;
+  *c_lo = __shfl(cq, kk - 1);
+  *c_hi = __shfl(cq, kk);
+}
+
+// One exact round: two cheap float rounds locate the transition approximately, then 64
+// lanes evaluate the exact CDF on q = ws .. ws+63 around it.  Returns false (caller runs
+// exact_search) unless the window provably brackets the reference's answer: the CDF is
+// strictly increasing for scale > 0, so the answer is the first q >= lower with
+// cdf(q) > mod, or lower + 2048 if no q <= lower + 2047 has one.
+__device__ __forceinline__ bool exact_window(uint64_t mod, int lower, float mi, float si, float lf,
+                                             int lane, int* s_out, int* c_lo, int* c_hi,
+                                             const uint64_t* tab, int g_sym = 0) {
+  const float rs = __frcp_rn(si);
+  const int64_t md = (int64_t)mod;
+  const int pa = lower + 32 * lane + 31;
+  STAMP(1);
+  const uint64_t ma = __ballot((int64_t)approx_cdf(pa, lower, mi, rs) > md);
+  const int blk = ma ? __ffsll((unsigned long long)ma) - 1 : 64;
+  const int pb = lower + 32 * blk - 32 + lane;  // block blk-1 and blk
+  const uint64_t mb = __ballot((int64_t)approx_cdf(pb, lower, mi, rs) > md);
+  const int sa = mb ? pb - lane + __ffsll((unsigned long long)mb) - 1 : pb - lane + 64;
+  STAMP(2);
+  int ws = sa - 32;
+  if (ws < lower - 1) ws = lower - 1;
+  if (ws > lower + 2048 - 63) ws = lower + 2048 - 63;
+  const int q = ws + lane;
+  const int cq = (IDF_DECODE_MODE != 2 && fast_scale_ok(si)) ? rans_cdf_rs(sym_x(q), mi, si, lf, tab, rcp_refined((double)si))
+                                   : rans_cdf(sym_x(q), mi, si, lf, tab);
+  const bool set = q > lower + 2047 || (int64_t)cq > md;
+  const uint64_t m = __ballot(set);
+  STAMP(3);
+  if ((m & 1ull) && ws >= lower) return false;  // answer may lie left of the window
+  const uint64_t m1 = m & ~1ull;
+  if (m1 == 0) return false;                       // answer right of the window
+  const int k = __ffsll((unsigned long long)m1) - 1;
+  *s_out = ws + k;
+  *c_lo = __shfl(cq, k - 1);
+  *c_hi = __shfl(cq, k);
+  STAMP(4);
+  return true;
 }
 
 __global__ void __launch_bounds__(64) rans_decode_kernel(
@@ -149,6 +339,9 @@ __global__ void __launch_bounds__(64) rans_decode_kernel(
     const float* __restrict__ mean, const float* __restrict__ scale,
     const uint64_t* __restrict__ init_state, uint64_t* __restrict__ final_state,
     float* __restrict__ out, int32_t* __restrict__ status) {
+  __shared__ uint64_t tab[32];
+  if (threadIdx.x < 32) tab[threadIdx.x] = kExp2fTab[threadIdx.x];
+  __syncthreads();
   const int64_t k = blockIdx.x;
   if (k >= nstreams) return;
   const int lane = threadIdx.x;
@@ -157,58 +350,90 @@ __global__ void __launch_bounds__(64) rans_decode_kernel(
   int64_t pos = nwords[k];
   uint64_t state = init_state[k];
   int32_t flag = 0;
-  for (int64_t j = 0; j < n; ++j) {
-    const int64_t i = b + n - 1 - j;
-    if (state < kRansL) {  // rans.pyx:86-89 (buffer read in reverse)
-      if (pos <= 0) {
-        flag |= IDF_STREAM_UNDERFLOW;
-        break;
-      }
-      state = (state << 32) | (uint64_t)w[--pos];
+  // Nothing the chain needs waits on memory: symbols are decoded in windows of 64 whose
+  // (mean, scale) sit one per lane (the next window's loads fly under this one), words
+  // come from a 64-word register window read with a uniform lane index, and each lane
+  // keeps its symbol's output for one coalesced store per window.
+  auto ld_params = [&](int64_t j0, float& mv, float& sv) {
+    const int64_t i = b + n - 1 - j0 - lane;  // reverse order
+    mv = 0.0f;
+    sv = 1.0f;
+    if (j0 + lane < n) {
+      mv = mean[i];
+      sv = scale[i];
     }
-    const uint64_t mod = state & 0xffffffull;
-    const float mi = mean[i], si = scale[i];
-    const int lower = rans_lower_int(mi);  // rans.pyx:91
-    const float lf = rans_lower_f(lower);  // rans.pyx:93
-    int s;
-    int c_lo, c_hi;
-    if (!(si > 0.0f)) {
-      if (si == 0.0f) {
-        flag |= IDF_STREAM_SCALE_ZERO;
-        break;
+  };
+  int64_t wbase = pos;  // lane l of wwin holds w[wbase - 1 - l]
+  uint32_t wwin = (wbase - 1 - lane >= 0) ? w[wbase - 1 - lane] : 0u;
+  float mcur, scur, mnxt = 0.0f, snxt = 1.0f;
+  ld_params(0, mcur, scur);
+  bool stop = false;
+  for (int64_t j0 = 0; j0 < n && !stop; j0 += 64) {
+    const int cnt = n - j0 < 64 ? (int)(n - j0) : 64;
+    if (j0 + 64 < n) ld_params(j0 + 64, mnxt, snxt);
+    float outv = 0.0f;
+    int done = 0;
+    for (int t = 0; t < cnt; ++t) {
+      if (state < kRansL) {  // rans.pyx:86-89 (buffer read in reverse)
+        if (pos <= 0) {
+          flag |= IDF_STREAM_UNDERFLOW;
+          stop = true;
+          break;
+        }
+        if (wbase - pos >= 64) {  // refill the word window
+          wbase = pos;
+          wwin = (wbase - 1 - lane >= 0) ? w[wbase - 1 - lane] : 0u;
+        }
+        const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)wwin, (int)(wbase - pos));
+        --pos;
+        state = (state << 32) | (uint64_t)word;
       }
-      s = ref_binary_search(mod, lower, mi, si, lf, &flag);
-      c_lo = rans_cdf(sym_x(s - 1), mi, si, lf);
-      c_hi = rans_cdf(sym_x(s), mi, si, lf);
-    } else {
-      // round 1: lane L probes the last bin of block L
-      int p1 = lower + 32 * lane + 31;
-      int c1 = rans_cdf(sym_x(p1), mi, si, lf);
-      uint64_t m1 = __ballot((uint64_t)(int64_t)c1 > mod);
-      if (m1 == 0) {
-        // no bin in the window has CDF > mod: reference leaves s = lower + 2048
-        s = lower + 2048;
-        int q = s - 1 + (lane & 1);
-        int cq = rans_cdf(sym_x(q), mi, si, lf);
-        c_lo = __shfl(cq, 0);
-        c_hi = __shfl(cq, 1);
-      } else {
-        int blk = __ffsll((unsigned long long)m1) - 1;
-        int base = lower + 32 * blk - 1;  // probe base-1 .. base+31 (33 points)
-        int q = base + (lane <= 32 ? lane : 32);
-        int cq = rans_cdf(sym_x(q), mi, si, lf);
-        uint64_t m2 = __ballot(lane >= 1 && lane <= 32 && (uint64_t)(int64_t)cq > mod);
-        int kk = __ffsll((unsigned long long)m2) - 1;  // >= 1
-        s = base + kk;
-        c_lo = __shfl(cq, kk - 1);
-        c_hi = __shfl(cq, kk);
+      const uint64_t mod = state & 0xffffffull;
+      { const int g_sym = (int)(j0 + t); (void)g_sym; STAMP(0); }
+      const float mi = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mcur), t));
+      const float si = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, scur), t));
+      const int lower = rans_lower_int(mi);  // rans.pyx:91
+      const float lf = rans_lower_f(lower);  // rans.pyx:93
+      int sym;
+      int c_lo, c_hi;
+      if (IDF_DECODE_MODE == 3 || IDF_DECODE_MODE == 4) {
+        sym = lower + (int)(mod & 1023);
+        if (IDF_DECODE_MODE == 4) {
+          const float rs = __frcp_rn(si);
+          const uint64_t ma = __ballot((int64_t)approx_cdf(lower + 32 * lane + 31, lower, mi, rs) > (int64_t)mod);
+          const int blk = ma ? __ffsll((unsigned long long)ma) - 1 : 64;
+          const uint64_t mb = __ballot((int64_t)approx_cdf(lower + 32 * blk - 32 + lane, lower, mi, rs) > (int64_t)mod);
+          sym += __ffsll((unsigned long long)mb);
+        }
+        c_lo = (int)(mod & 0xFFFFF);
+        c_hi = c_lo + 1000;
+      } else if (!(si > 0.0f)) {
+        if (si == 0.0f) {
+          flag |= IDF_STREAM_SCALE_ZERO;
+          stop = true;
+          break;
+        }
+        sym = ref_binary_search(mod, lower, mi, si, lf, &flag, tab);
+        c_lo = rans_cdf(sym_x(sym - 1), mi, si, lf, tab);
+        c_hi = rans_cdf(sym_x(sym), mi, si, lf, tab);
+      } else if (IDF_DECODE_MODE == 1 ||
+                 !exact_window(mod, lower, mi, si, lf, lane, &sym, &c_lo, &c_hi, tab, (int)(j0 + t))) {
+#if IDF_DECODE_MODE == 5
+        if (lane == 0) atomicAdd(&g_decode_fallbacks, 1ull);
+#endif
+        exact_search(mod, lower, mi, si, lf, lane, &sym, &c_lo, &c_hi, tab);
       }
+      if (c_lo < 0 || c_hi - c_lo < 0) flag |= IDF_STREAM_NEG_CDF;
+      const uint64_t cdf_s = (uint64_t)(int64_t)c_lo;
+      const uint64_t freq_s = (uint64_t)(int64_t)(c_hi - c_lo);
+      state = (state >> 24) * freq_s + (state & 0xffffffull) - cdf_s;  // rans.pyx:108
+      if (lane == t) outv = sym_x(sym);  // message.push_back(s / 256.)
+      done = t + 1;
+      { const int g_sym = (int)(j0 + t); (void)g_sym; STAMP(5); }
     }
-    if (c_lo < 0 || c_hi - c_lo < 0) flag |= IDF_STREAM_NEG_CDF;
-    const uint64_t cdf_s = (uint64_t)(int64_t)c_lo;
-    const uint64_t freq_s = (uint64_t)(int64_t)(c_hi - c_lo);
-    state = (state >> 24) * freq_s + (state & 0xffffffull) - cdf_s;  // rans.pyx:108
-    if (lane == 0) out[i] = sym_x(s);  // message.push_back(s / 256.)
+    if (lane < done) out[b + n - 1 - j0 - lane] = outv;
+    mcur = mnxt;
+    scur = snxt;
   }
   if (lane == 0) {
     final_state[k] = state;
@@ -252,6 +477,35 @@ __global__ void __launch_bounds__(256) expf_checksum_kernel(uint64_t lo, uint64_
   if ((threadIdx.x & 63) == 0) atomicAdd(acc, sum);
 }
 
+// Self-check of rans_cdf_rs against rans_cdf on pseudo-random (x, mean, scale): scale
+// log-uniform over the fast range, mean in +-2^12, x on the 1/256 grid within the
+// window around mean.  Counts mismatching CDF values.
+__global__ void __launch_bounds__(256) cdf_selfcheck_kernel(uint64_t n, uint64_t seed,
+                                                            unsigned long long* bad) {
+  __shared__ uint64_t tab[32];
+  if (threadIdx.x < 32) tab[threadIdx.x] = kExp2fTab[threadIdx.x];
+  __syncthreads();
+  unsigned long long cnt = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    uint64_t h = (i + seed) * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 31; h *= 0xBF58476D1CE4E5B9ull; h ^= h >> 29;
+    const float e = (float)((h & 0xFFFF) / 65536.0) * 120.0f - 60.0f;  // scale = 2^e
+    const float scale = exp2f(e);
+    const float mean = (float)(((h >> 16) & 0xFFFFFF) / 16777216.0 * 8192.0 - 4096.0);
+    const int lower = rans_lower_int(mean);
+    const float lf = rans_lower_f(lower);
+    const int sidx = lower - 1 + (int)((h >> 40) % 2050u);
+    const float x = (float)((double)sidx / 256.0);
+    if (!fast_scale_ok(scale)) continue;
+    const int a = rans_cdf(x, mean, scale, lf, tab);
+    const int b = rans_cdf_rs(x, mean, scale, lf, tab, rcp_refined((double)scale));
+    cnt += (a != b);
+  }
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_down(cnt, o);
+  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(bad, cnt);
+}
+
 }  // namespace idf
 
 // ============================================================== C-ABI
@@ -270,7 +524,7 @@ int idf_rans_cdf_freq(void* stream, int64_t n, const float* x, const float* mean
 }
 
 int64_t idf_rans_encode_workspace_bytes(int64_t nsym) {
-  return 2 * (int64_t)sizeof(int32_t) * (nsym > 0 ? nsym : 1);
+  return (int64_t)(sizeof(EncSym) + sizeof(double)) * (nsym > 0 ? nsym : 1);
 }
 
 int idf_rans_encode_streams(void* stream, int64_t nstreams, int64_t nsym, const int64_t* sym_off,
@@ -281,14 +535,16 @@ int idf_rans_encode_streams(void* stream, int64_t nstreams, int64_t nsym, const 
   if (nstreams < 0 || nsym < 0) return IDF_ERR_ARG;
   if (nstreams == 0) return IDF_OK;
   if (workspace_bytes < idf_rans_encode_workspace_bytes(nsym)) return IDF_ERR_WORKSPACE;
-  int32_t* st = (int32_t*)workspace;
-  int32_t* fr = st + (nsym > 0 ? nsym : 1);
-  int rc = idf_rans_cdf_freq(stream, nsym, x, mean, scale, st, fr);
+  EncSym* es = (EncSym*)workspace;
+  double* rcp = (double*)(es + (nsym > 0 ? nsym : 1));
+  int rc = IDF_OK;
+  if (nsym > 0)
+    hipLaunchKernelGGL(rans_encode_prep_kernel, dim3((unsigned)((nsym + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, nsym, x, mean, scale, es, rcp);
   if (rc) return rc;
   int64_t blocks = (nstreams + 63) / 64;
   hipLaunchKernelGGL(rans_encode_kernel, dim3((unsigned)blocks), dim3(64), 0, (hipStream_t)stream,
-                     nstreams, sym_off, x, mean, st, fr, init_state, final_state, words, nwords,
-                     status);
+                     nstreams, sym_off, es, rcp, init_state, final_state, words, nwords, status);
   return idf_last_error();
 }
 
@@ -317,6 +573,12 @@ int idf_expf_glibc(void* stream, int64_t n, const float* in, float* out) {
   if (n <= 0) return n < 0 ? IDF_ERR_ARG : IDF_OK;
   hipLaunchKernelGGL(expf_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, n, in, out);
+  return idf_last_error();
+}
+
+int idf_rans_cdf_selfcheck(void* stream, uint64_t n, uint64_t seed, unsigned long long* bad) {
+  hipLaunchKernelGGL(cdf_selfcheck_kernel, dim3(4096), dim3(256), 0, (hipStream_t)stream, n, seed,
+                     bad);
   return idf_last_error();
 }
 

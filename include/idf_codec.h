@@ -93,6 +93,9 @@ int idf_rans_decode(uint64_t *state_io, const uint32_t *words, int64_t nwords, i
  * rans.pyx:6-9); exposed for the parity tests. */
 int idf_expf_glibc(void *stream, int64_t n, const float *d_in, float *d_out);
 int idf_expf_checksum(void *stream, uint64_t lo, uint64_t hi, unsigned long long *d_acc);
+/* Decoder self-check: the decode window's CDF (divisions with a hoisted reciprocal)
+ * against the plain CDF on n pseudo-random (x, mean, scale); adds mismatches to *d_bad. */
+int idf_rans_cdf_selfcheck(void *stream, uint64_t n, uint64_t seed, unsigned long long *d_bad);
 
 /* ======================================================================== *
  * Flow operators (integer-discrete flow, fp32).  Activations are stored

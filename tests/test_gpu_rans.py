@@ -199,3 +199,12 @@ def test_device_expf_exhaustive_checksum(tmp_path):
     check(lib().idf_expf_checksum(_lib.stream_ptr(), 0, 1 << 32, ptr(acc)), "checksum")
     dev_sum = int(np.int64(acc.item()).view(np.uint64))
     assert dev_sum == host_sum
+
+
+def test_decode_window_cdf_matches_plain_cdf():
+    """The decoder's CDF with hoisted reciprocals == rans_cdf bit for bit (2^26 samples)."""
+    from idfcodec import _lib
+    from idfcodec._lib import check, lib, ptr
+    bad = torch.zeros(1, dtype=torch.int64, device="cuda")
+    check(lib().idf_rans_cdf_selfcheck(_lib.stream_ptr(), 1 << 26, 12345, ptr(bad)), "selfcheck")
+    assert int(bad.item()) == 0
