@@ -16,8 +16,8 @@
 //                     symbol records loaded 8 ahead of the chain.
 //   rans_decode     : rans.pyx:69-110, ONE WAVE per stream.  The reference's
 //                     11-12 step binary search over the 2048-bin window is
-//                     replaced by ONE round of 64 exact CDF probes placed by two
-//                     cheap float rounds (exact_window), with a two-round exact
+//                     replaced by ONE round of 64 exact CDF probes placed by a
+//                     cheap float round (exact_window), with a two-round exact
 //                     64-ary search (exact_search) whenever the window does not
 //                     provably bracket the answer.  The CDF is strictly increasing
 //                     in s for scale > 0 (part2 steps by 1, part1 is monotone:
@@ -280,8 +280,8 @@ __device__ __forceinline__ void exact_search(uint64_t mod, int lower, float mi, 
     int q = s - 1 + (lane & 1);
     int cq = rans_cdf(sym_x(q), mi, si, lf, tab);
     *s_out = s;
-    *c_lo = __shfl(cq, 0);
-    *c_hi = __shfl(cq, 1);
+    *c_lo = __builtin_amdgcn_readlane(cq, 0);
+    *c_hi = __builtin_amdgcn_readlane(cq, 1);
     return;
   }
   int blk = __ffsll((unsigned long long)m1) - 1;
@@ -291,34 +291,46 @@ __device__ __forceinline__ void exact_search(uint64_t mod, int lower, float mi, 
   uint64_t m2 = __ballot(lane >= 1 && lane <= 32 && (uint64_t)(int64_t)cq > mod);
   int kk = __ffsll((unsigned long long)m2) - 1;  // >= 1
   *s_out = base + kk;
-  *c_lo = __shfl(cq, kk - 1);
-  *c_hi = __shfl(cq, kk);
+  *c_lo = __builtin_amdgcn_readlane(cq, kk - 1);
+  *c_hi = __builtin_amdgcn_readlane(cq, kk);
 }
 
-// One exact round: two cheap float rounds locate the transition approximately, then 64
-// lanes evaluate the exact CDF on q = ws .. ws+63 around it.  Returns false (caller runs
-// exact_search) unless the window provably brackets the reference's answer: the CDF is
-// strictly increasing for scale > 0, so the answer is the first q >= lower with
-// cdf(q) > mod, or lower + 2048 if no q <= lower + 2047 has one.
+// Decode pass 1 (fully parallel, off the serial chain): for every symbol, the float
+// estimate of the CDF at the last bin of each of the window's 64 blocks of 32 bins.
+// btab[i * 64 + l] = approx_cdf(lower_i + 32 l + 31).
+__global__ void __launch_bounds__(256) rans_decode_prep_kernel(int64_t n, const float* __restrict__ mean,
+                                                               const float* __restrict__ scale,
+                                                               int32_t* __restrict__ btab) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = g >> 6;
+  const int l = (int)(g & 63);
+  if (i >= n) return;
+  const float mi = mean[i], si = scale[i];
+  const int lower = rans_lower_int(mi);
+  btab[g] = approx_cdf(lower + 32 * l + 31, lower, mi, __builtin_amdgcn_rcpf(si));
+}
+
+// One exact round: the precomputed block estimates (ablk: this lane's block) locate the
+// transition's 32-bin block, then 64 lanes evaluate the exact CDF on q = ws .. ws+63
+// centred on it.  Returns false (caller runs exact_search) unless the window provably
+// brackets the reference's answer: the CDF is strictly increasing for scale > 0, so the
+// answer is the first q >= lower with cdf(q) > mod, or lower + 2048 if no q <= lower + 2047
+// has one.  rs = rcp_refined(scale) when fast_scale_ok(scale).
 __device__ __forceinline__ bool exact_window(uint64_t mod, int lower, float mi, float si, float lf,
-                                             int lane, int* s_out, int* c_lo, int* c_hi,
-                                             const uint64_t* tab, int g_sym = 0) {
-  const float rs = __frcp_rn(si);
+                                             double rs, int ablk, int lane, int* s_out, int* c_lo,
+                                             int* c_hi, const uint64_t* tab, int g_sym = 0) {
   const int64_t md = (int64_t)mod;
-  const int pa = lower + 32 * lane + 31;
   STAMP(1);
-  const uint64_t ma = __ballot((int64_t)approx_cdf(pa, lower, mi, rs) > md);
+  const uint64_t ma = __ballot((int64_t)ablk > md);
   const int blk = ma ? __ffsll((unsigned long long)ma) - 1 : 64;
-  const int pb = lower + 32 * blk - 32 + lane;  // block blk-1 and blk
-  const uint64_t mb = __ballot((int64_t)approx_cdf(pb, lower, mi, rs) > md);
-  const int sa = mb ? pb - lane + __ffsll((unsigned long long)mb) - 1 : pb - lane + 64;
   STAMP(2);
-  int ws = sa - 32;
+  int ws = lower + 32 * blk + 16 - 32;  // the window is centred on the block
   if (ws < lower - 1) ws = lower - 1;
   if (ws > lower + 2048 - 63) ws = lower + 2048 - 63;
   const int q = ws + lane;
-  const int cq = (IDF_DECODE_MODE != 2 && fast_scale_ok(si)) ? rans_cdf_rs(sym_x(q), mi, si, lf, tab, rcp_refined((double)si))
-                                   : rans_cdf(sym_x(q), mi, si, lf, tab);
+  const int cq = (IDF_DECODE_MODE != 2 && fast_scale_ok(si))
+                     ? rans_cdf_rs(sym_x(q), mi, si, lf, tab, rs)
+                     : rans_cdf(sym_x(q), mi, si, lf, tab);
   const bool set = q > lower + 2047 || (int64_t)cq > md;
   const uint64_t m = __ballot(set);
   STAMP(3);
@@ -327,8 +339,8 @@ __device__ __forceinline__ bool exact_window(uint64_t mod, int lower, float mi, 
   if (m1 == 0) return false;                       // answer right of the window
   const int k = __ffsll((unsigned long long)m1) - 1;
   *s_out = ws + k;
-  *c_lo = __shfl(cq, k - 1);
-  *c_hi = __shfl(cq, k);
+  *c_lo = __builtin_amdgcn_readlane(cq, k - 1);  // k is wave-uniform
+  *c_hi = __builtin_amdgcn_readlane(cq, k);
   STAMP(4);
   return true;
 }
@@ -338,8 +350,9 @@ __global__ void __launch_bounds__(64) rans_decode_kernel(
     const int64_t* __restrict__ nwords, const uint32_t* __restrict__ words,
     const float* __restrict__ mean, const float* __restrict__ scale,
     const uint64_t* __restrict__ init_state, uint64_t* __restrict__ final_state,
-    float* __restrict__ out, int32_t* __restrict__ status) {
+    float* __restrict__ out, int32_t* __restrict__ status, const int32_t* __restrict__ btab) {
   __shared__ uint64_t tab[32];
+  __shared__ __attribute__((aligned(16))) int32_t bt[2][64 * 64];  // block estimates, 2 windows
   if (threadIdx.x < 32) tab[threadIdx.x] = kExp2fTab[threadIdx.x];
   __syncthreads();
   const int64_t k = blockIdx.x;
@@ -351,9 +364,11 @@ __global__ void __launch_bounds__(64) rans_decode_kernel(
   uint64_t state = init_state[k];
   int32_t flag = 0;
   // Nothing the chain needs waits on memory: symbols are decoded in windows of 64 whose
-  // (mean, scale) sit one per lane (the next window's loads fly under this one), words
-  // come from a 64-word register window read with a uniform lane index, and each lane
-  // keeps its symbol's output for one coalesced store per window.
+  // (mean, scale) and derived (lower, 1/scale) sit one per lane, computed in parallel
+  // while the previous window decodes; the window's block estimates are copied into LDS
+  // by DMA one window ahead; words come from a 64-word register window read with a
+  // uniform lane index; each lane keeps its symbol's output for one coalesced store per
+  // window.
   auto ld_params = [&](int64_t j0, float& mv, float& sv) {
     const int64_t i = b + n - 1 - j0 - lane;  // reverse order
     mv = 0.0f;
@@ -363,73 +378,94 @@ __global__ void __launch_bounds__(64) rans_decode_kernel(
       sv = scale[i];
     }
   };
+  // window at j0 -> bt[slot][t * 64 + l] = btab[(i_hi - t) * 64 + l], i_hi = b + n - 1 - j0
+  auto ld_blk = [&](int64_t j0, int slot) {
+    const int cnt = n - j0 < 64 ? (int)(n - j0) : 64;
+    for (int t = 0; t < cnt; t += 4) {  // 4 symbols (1 KiB) per DMA wave-instruction
+      const int tl = t + (lane >> 4);
+      const int64_t i = b + n - 1 - j0 - (tl < cnt ? tl : cnt - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(btab + i * 64 + 4 * (lane & 15)),
+                                       (__attribute__((address_space(3))) void*)(&bt[slot][t * 64]),
+                                       16, 0, 0);
+    }
+  };
   int64_t wbase = pos;  // lane l of wwin holds w[wbase - 1 - l]
   uint32_t wwin = (wbase - 1 - lane >= 0) ? w[wbase - 1 - lane] : 0u;
   float mcur, scur, mnxt = 0.0f, snxt = 1.0f;
   ld_params(0, mcur, scur);
+  asm volatile("" ::"v"(wwin), "v"(mcur), "v"(scur));
+  if (n > 0) ld_blk(0, 0);
   bool stop = false;
-  for (int64_t j0 = 0; j0 < n && !stop; j0 += 64) {
+  int slot = 0;
+  for (int64_t j0 = 0; j0 < n && !stop; j0 += 64, slot ^= 1) {
     const int cnt = n - j0 < 64 ? (int)(n - j0) : 64;
-    if (j0 + 64 < n) ld_params(j0 + 64, mnxt, snxt);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this window's estimates have landed
+    if (j0 + 64 < n) {
+      ld_blk(j0 + 64, slot ^ 1);
+      ld_params(j0 + 64, mnxt, snxt);
+    }
+    // per-lane derived parameters of this window's symbols
+    const int lower_l = rans_lower_int(mcur);  // rans.pyx:91
+    const float lf_l = rans_lower_f(lower_l);  // rans.pyx:93
+    const double rs_l = fast_scale_ok(scur) ? rcp_refined((double)scur) : 0.0;
     float outv = 0.0f;
     int done = 0;
-    for (int t = 0; t < cnt; ++t) {
-      if (state < kRansL) {  // rans.pyx:86-89 (buffer read in reverse)
-        if (pos <= 0) {
-          flag |= IDF_STREAM_UNDERFLOW;
-          stop = true;
-          break;
+    {
+      for (int t = 0; t < cnt; ++t) {
+        const int ablk = bt[slot][t * 64 + lane];
+        if (state < kRansL) {  // rans.pyx:86-89 (buffer read in reverse)
+          if (pos <= 0) {
+            flag |= IDF_STREAM_UNDERFLOW;
+            stop = true;
+            break;
+          }
+          if (wbase - pos >= 64) {  // refill the word window
+            wbase = pos;
+            wwin = (wbase - 1 - lane >= 0) ? w[wbase - 1 - lane] : 0u;
+            // wait for it here, so the readlanes below never wait on the block estimates
+            asm volatile("" ::"v"(wwin));
+          }
+          const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)wwin, (int)(wbase - pos));
+          --pos;
+          state = (state << 32) | (uint64_t)word;
         }
-        if (wbase - pos >= 64) {  // refill the word window
-          wbase = pos;
-          wwin = (wbase - 1 - lane >= 0) ? w[wbase - 1 - lane] : 0u;
-        }
-        const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)wwin, (int)(wbase - pos));
-        --pos;
-        state = (state << 32) | (uint64_t)word;
-      }
-      const uint64_t mod = state & 0xffffffull;
-      { const int g_sym = (int)(j0 + t); (void)g_sym; STAMP(0); }
-      const float mi = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mcur), t));
-      const float si = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, scur), t));
-      const int lower = rans_lower_int(mi);  // rans.pyx:91
-      const float lf = rans_lower_f(lower);  // rans.pyx:93
-      int sym;
-      int c_lo, c_hi;
-      if (IDF_DECODE_MODE == 3 || IDF_DECODE_MODE == 4) {
-        sym = lower + (int)(mod & 1023);
-        if (IDF_DECODE_MODE == 4) {
-          const float rs = __frcp_rn(si);
-          const uint64_t ma = __ballot((int64_t)approx_cdf(lower + 32 * lane + 31, lower, mi, rs) > (int64_t)mod);
-          const int blk = ma ? __ffsll((unsigned long long)ma) - 1 : 64;
-          const uint64_t mb = __ballot((int64_t)approx_cdf(lower + 32 * blk - 32 + lane, lower, mi, rs) > (int64_t)mod);
-          sym += __ffsll((unsigned long long)mb);
-        }
-        c_lo = (int)(mod & 0xFFFFF);
-        c_hi = c_lo + 1000;
-      } else if (!(si > 0.0f)) {
-        if (si == 0.0f) {
-          flag |= IDF_STREAM_SCALE_ZERO;
-          stop = true;
-          break;
-        }
-        sym = ref_binary_search(mod, lower, mi, si, lf, &flag, tab);
-        c_lo = rans_cdf(sym_x(sym - 1), mi, si, lf, tab);
-        c_hi = rans_cdf(sym_x(sym), mi, si, lf, tab);
-      } else if (IDF_DECODE_MODE == 1 ||
-                 !exact_window(mod, lower, mi, si, lf, lane, &sym, &c_lo, &c_hi, tab, (int)(j0 + t))) {
+        const uint64_t mod = state & 0xffffffull;
+        { const int g_sym = (int)(j0 + t); (void)g_sym; STAMP(0); }
+        const float mi = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mcur), t));
+        const float si = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, scur), t));
+        const int lower = __builtin_amdgcn_readlane(lower_l, t);
+        const float lf = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lf_l), t));
+        const uint64_t rsb = __builtin_bit_cast(uint64_t, rs_l);
+        const double rs = __builtin_bit_cast(
+            double, ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(rsb >> 32), t) << 32) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rsb, t));
+        int sym;
+        int c_lo, c_hi;
+        if (!(si > 0.0f)) {
+          if (si == 0.0f) {
+            flag |= IDF_STREAM_SCALE_ZERO;
+            stop = true;
+            break;
+          }
+          sym = ref_binary_search(mod, lower, mi, si, lf, &flag, tab);
+          c_lo = rans_cdf(sym_x(sym - 1), mi, si, lf, tab);
+          c_hi = rans_cdf(sym_x(sym), mi, si, lf, tab);
+        } else if (IDF_DECODE_MODE == 1 ||
+                   !exact_window(mod, lower, mi, si, lf, rs, ablk, lane, &sym, &c_lo, &c_hi, tab,
+                                 (int)(j0 + t))) {
 #if IDF_DECODE_MODE == 5
-        if (lane == 0) atomicAdd(&g_decode_fallbacks, 1ull);
+          if (lane == 0) atomicAdd(&g_decode_fallbacks, 1ull);
 #endif
-        exact_search(mod, lower, mi, si, lf, lane, &sym, &c_lo, &c_hi, tab);
+          exact_search(mod, lower, mi, si, lf, lane, &sym, &c_lo, &c_hi, tab);
+        }
+        if (c_lo < 0 || c_hi - c_lo < 0) flag |= IDF_STREAM_NEG_CDF;
+        const uint64_t cdf_s = (uint64_t)(int64_t)c_lo;
+        const uint64_t freq_s = (uint64_t)(int64_t)(c_hi - c_lo);
+        state = (state >> 24) * freq_s + (state & 0xffffffull) - cdf_s;  // rans.pyx:108
+        if (lane == t) outv = sym_x(sym);  // message.push_back(s / 256.)
+        done = t + 1;
+        { const int g_sym = (int)(j0 + t); (void)g_sym; STAMP(5); }
       }
-      if (c_lo < 0 || c_hi - c_lo < 0) flag |= IDF_STREAM_NEG_CDF;
-      const uint64_t cdf_s = (uint64_t)(int64_t)c_lo;
-      const uint64_t freq_s = (uint64_t)(int64_t)(c_hi - c_lo);
-      state = (state >> 24) * freq_s + (state & 0xffffffull) - cdf_s;  // rans.pyx:108
-      if (lane == t) outv = sym_x(sym);  // message.push_back(s / 256.)
-      done = t + 1;
-      { const int g_sym = (int)(j0 + t); (void)g_sym; STAMP(5); }
     }
     if (lane < done) out[b + n - 1 - j0 - lane] = outv;
     mcur = mnxt;
@@ -548,15 +584,25 @@ int idf_rans_encode_streams(void* stream, int64_t nstreams, int64_t nsym, const 
   return idf_last_error();
 }
 
-int idf_rans_decode_streams(void* stream, int64_t nstreams, const int64_t* sym_off,
+int64_t idf_rans_decode_workspace_bytes(int64_t nsym) {
+  return 64 * (int64_t)sizeof(int32_t) * (nsym > 0 ? nsym : 1);
+}
+
+int idf_rans_decode_streams(void* stream, int64_t nstreams, int64_t nsym, const int64_t* sym_off,
                             const int64_t* word_off, const int64_t* nwords, const uint32_t* words,
                             const float* mean, const float* scale, const uint64_t* init_state,
-                            uint64_t* final_state, float* out, int32_t* status) {
-  if (nstreams < 0) return IDF_ERR_ARG;
+                            uint64_t* final_state, float* out, int32_t* status, void* workspace,
+                            int64_t workspace_bytes) {
+  if (nstreams < 0 || nsym < 0) return IDF_ERR_ARG;
   if (nstreams == 0) return IDF_OK;
+  if (workspace_bytes < idf_rans_decode_workspace_bytes(nsym)) return IDF_ERR_WORKSPACE;
+  int32_t* btab = (int32_t*)workspace;
+  if (nsym > 0)
+    hipLaunchKernelGGL(rans_decode_prep_kernel, dim3((unsigned)((nsym * 64 + 255) / 256)), dim3(256),
+                       0, (hipStream_t)stream, nsym, mean, scale, btab);
   hipLaunchKernelGGL(rans_decode_kernel, dim3((unsigned)nstreams), dim3(64), 0,
                      (hipStream_t)stream, nstreams, sym_off, word_off, nwords, words, mean, scale,
-                     init_state, final_state, out, status);
+                     init_state, final_state, out, status, btab);
   return idf_last_error();
 }
 
@@ -646,7 +692,7 @@ int idf_rans_decode(uint64_t* state_io, const uint32_t* words, int64_t nwords, i
   int64_t nn = n > 0 ? n : 1, nwn = nwords > 0 ? nwords : 1;
   int rc = IDF_OK;
   char* dbuf = nullptr;
-  size_t bytes = 3 * nn * 4 + nwn * 4 + 16 + 8 * 4 + 4 + 128;
+  size_t bytes = 3 * nn * 4 + nwn * 4 + 16 + 8 * 4 + 4 + 256 + (size_t)idf_rans_decode_workspace_bytes(n);
   if (hipMalloc(&dbuf, bytes) != hipSuccess) return IDF_ERR_HIP;
   char* p = dbuf;
   auto take = [&](size_t b) { char* r = p; p += (b + 15) & ~(size_t)15; return r; };
@@ -660,6 +706,7 @@ int idf_rans_decode(uint64_t* state_io, const uint32_t* words, int64_t nwords, i
   uint64_t* dst = (uint64_t*)take(8);
   uint64_t* dfs = (uint64_t*)take(8);
   int32_t* dstat = (int32_t*)take(4);
+  void* dws = take((size_t)idf_rans_decode_workspace_bytes(n));
   int64_t off[2] = {0, n}, zero = 0;
   if (n > 0) {
     CK(hipMemcpy(dm, mean, n * 4, hipMemcpyHostToDevice));
@@ -670,7 +717,9 @@ int idf_rans_decode(uint64_t* state_io, const uint32_t* words, int64_t nwords, i
   CK(hipMemcpy(dwoff, &zero, 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(dnw, &nwords, 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(dst, state_io, 8, hipMemcpyHostToDevice));
-  if (rc == IDF_OK) rc = idf_rans_decode_streams(nullptr, 1, doff, dwoff, dnw, dw, dm, ds, dst, dfs, dout, dstat);
+  if (rc == IDF_OK)
+    rc = idf_rans_decode_streams(nullptr, 1, n, doff, dwoff, dnw, dw, dm, ds, dst, dfs, dout, dstat, dws,
+                                 idf_rans_decode_workspace_bytes(n));
   int32_t stat = 0;
   if (rc == IDF_OK) {
     CK(hipMemcpy(state_io, dfs, 8, hipMemcpyDeviceToHost));

@@ -69,7 +69,8 @@ SIGNATURES = {
     "idf_rans_cdf_freq": (ctypes.c_int, [P, i64, P, P, P, P, P]),
     "idf_rans_encode_workspace_bytes": (i64, [i64]),
     "idf_rans_encode_streams": (ctypes.c_int, [P, i64, i64, P, P, P, P, P, P, P, P, P, P, i64]),
-    "idf_rans_decode_streams": (ctypes.c_int, [P, i64, P, P, P, P, P, P, P, P, P, P]),
+    "idf_rans_decode_workspace_bytes": (i64, [i64]),
+    "idf_rans_decode_streams": (ctypes.c_int, [P, i64, i64, P, P, P, P, P, P, P, P, P, P, P, i64]),
     "idf_gather_words": (ctypes.c_int, [P, i64, P, P, P, P, P]),
     "idf_rans_encode": (ctypes.c_int, [P, i64, P, P, P, P, P, P]),
     "idf_rans_decode": (ctypes.c_int, [P, P, i64, i64, P, P, P, P]),

@@ -101,6 +101,8 @@ class StreamCoder:
     def __init__(self, engine):
         self.engine = engine
         self._off = {}
+        self._lvl = {}
+        self._dws = None
 
     def sym_off(self, B: int) -> torch.Tensor:
         t = self._off.get(B)
@@ -147,16 +149,32 @@ class StreamCoder:
                                      ptr(words)), "gather words")
         return Bitstream(B, shapes, final, nwords, words[:total], status, meta=meta)
 
+    def level_streams(self, B: int, l: int):
+        """(first symbol of level l, its symbol count, device int64[B+1] stream offsets
+        relative to that first symbol) -- a level's decode touches only its own symbols."""
+        key = (B, l)
+        hit = self._lvl.get(key)
+        if hit is None:
+            base = B * sum(L.n_sym for L in self.engine.levels[:l])
+            n = self.engine.levels[l].n_sym
+            rel = torch.arange(B + 1, dtype=torch.int64, device=self.engine.device) * n
+            hit = (base, B * n, rel)
+            self._lvl[key] = hit
+        return hit
+
     def decode_level(self, bs: Bitstream, B: int, l: int, ws, word_off, out_state, out_status):
         eng = self.engine
         s = _lib.stream_ptr(eng.device)
-        off = self.sym_off(B)
-        k0, k1 = l * B, (l + 1) * B
+        base, nsym, rel = self.level_streams(B, l)
+        k0 = l * B
+        wbytes = lib().idf_rans_decode_workspace_bytes(nsym)
+        if self._dws is None or self._dws.numel() < wbytes:
+            self._dws = torch.empty(wbytes, dtype=torch.uint8, device=eng.device)
         check(lib().idf_rans_decode_streams(
-            s, B, ptr(off) + 8 * k0, ptr(word_off) + 8 * k0, ptr(bs.nwords) + 8 * k0, ptr(bs.words),
-            ptr(ws["mean"]), ptr(ws["scale"]), ptr(bs.states) + 8 * k0, ptr(out_state) + 8 * k0,
-            ptr(ws["lat"]), ptr(out_status) + 4 * k0), "rans decode")
-        del k1
+            s, B, nsym, ptr(rel), ptr(word_off) + 8 * k0, ptr(bs.nwords) + 8 * k0, ptr(bs.words),
+            ptr(ws["mean"]) + 4 * base, ptr(ws["scale"]) + 4 * base, ptr(bs.states) + 8 * k0,
+            ptr(out_state) + 8 * k0, ptr(ws["lat"]) + 4 * base, ptr(out_status) + 4 * k0,
+            ptr(self._dws), wbytes), "rans decode")
 
 
 class ImageCodec:

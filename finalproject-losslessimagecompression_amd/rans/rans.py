@@ -101,9 +101,11 @@ def decode(state, buffer_, n, mean_, scale_):
     final = torch.empty(1, dtype=torch.int64, device=dev)
     out = torch.empty(n, dtype=torch.float32, device=dev)
     status = torch.empty(1, dtype=torch.int32, device=dev)
-    check(lib().idf_rans_decode_streams(_lib.stream_ptr(dev), 1, ptr(off), ptr(woff), ptr(nw),
+    wb = lib().idf_rans_decode_workspace_bytes(n)
+    ws = torch.empty(wb, dtype=torch.uint8, device=dev)
+    check(lib().idf_rans_decode_streams(_lib.stream_ptr(dev), 1, n, ptr(off), ptr(woff), ptr(nw),
                                         ptr(dw), ptr(dm), ptr(ds), ptr(init), ptr(final), ptr(out),
-                                        ptr(status)), "rans decode")
+                                        ptr(status), ptr(ws), wb), "rans decode")
     _raise_status(int(status.item()))
     st = int(np.int64(final.item()).view(np.uint64))
     return st, out.cpu().numpy()[::-1].astype(np.float64).tolist()

@@ -69,12 +69,15 @@ int idf_rans_encode_streams(void *stream, int64_t nstreams, int64_t nsym, const 
 /* Decode many independent streams.  Replaces rans.pyx:69-110 (`decode`).
  * Words of stream k: d_words + d_word_off[k], d_nwords[k] of them in PUSH order
  * (the reference's reversed buffer_ is read from the end here); mean/scale/out
- * in natural symbol order (the reference's reversals folded into indexing). */
-int idf_rans_decode_streams(void *stream, int64_t nstreams, const int64_t *d_sym_off,
+ * in natural symbol order (the reference's reversals folded into indexing).
+ * nsym bounds the symbol indices (d_sym_off[nstreams] <= nsym); the workspace
+ * (idf_rans_decode_workspace_bytes(nsym)) holds per-symbol search estimates. */
+int64_t idf_rans_decode_workspace_bytes(int64_t nsym);
+int idf_rans_decode_streams(void *stream, int64_t nstreams, int64_t nsym, const int64_t *d_sym_off,
                             const int64_t *d_word_off, const int64_t *d_nwords,
                             const uint32_t *d_words, const float *d_mean, const float *d_scale,
                             const uint64_t *d_init_state, uint64_t *d_final_state, float *d_out,
-                            int32_t *d_status);
+                            int32_t *d_status, void *d_workspace, int64_t workspace_bytes);
 
 /* Compact per-stream word runs: dst[dst_off[k] + i] = src[src_off[k] + i], i < nwords[k]. */
 int idf_gather_words(void *stream, int64_t nstreams, const int64_t *d_src_off,

@@ -54,8 +54,11 @@ def _dec_streams(off, woff, nw, words, mean, scale, init):
     bufs = [t(off, torch.int64), t(woff, torch.int64), t(nw, torch.int64), w,
             t(mean, torch.float32), t(scale, torch.float32),
             t(np.asarray(init, np.uint64).view(np.int64), torch.int64)]
-    check(lib().idf_rans_decode_streams(_lib.stream_ptr(), ns, *[ptr(b) for b in bufs],
-                                        ptr(fs), ptr(out), ptr(st)), "dec")
+    nsym = int(off[-1])
+    wb = lib().idf_rans_decode_workspace_bytes(nsym)
+    ws = torch.empty(wb, dtype=torch.uint8, device=dev)
+    check(lib().idf_rans_decode_streams(_lib.stream_ptr(), ns, nsym, *[ptr(b) for b in bufs],
+                                        ptr(fs), ptr(out), ptr(st), ptr(ws), wb), "dec")
     torch.cuda.synchronize()
     return fs.cpu().numpy().view(np.uint64), out.cpu().numpy()[: int(off[-1])], st.cpu().numpy()
 

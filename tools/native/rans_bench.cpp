@@ -37,6 +37,8 @@ int main(int argc, char** argv) {
   CKH(hipMalloc(&dwoff, S * 8)); CKH(hipMalloc(&dinit, S * 8)); CKH(hipMalloc(&dfin, S * 8));
   CKH(hipMalloc(&dfin2, S * 8)); CKH(hipMalloc(&dw, n * 4)); CKH(hipMalloc(&dst, S * 4));
   CKH(hipMalloc(&dst2, S * 4)); CKH(hipMalloc(&ws, wsb));
+  void* dws;
+  CKH(hipMalloc(&dws, idf_rans_decode_workspace_bytes(n)));
   CKH(hipMemcpy(dx, x.data(), n * 4, hipMemcpyHostToDevice));
   CKH(hipMemcpy(dm, mean.data(), n * 4, hipMemcpyHostToDevice));
   CKH(hipMemcpy(ds, scale.data(), n * 4, hipMemcpyHostToDevice));
@@ -57,7 +59,8 @@ int main(int argc, char** argv) {
     CKH(hipEventElapsedTime(&ms, e0, e1));
     if (ms < enc_best) enc_best = ms;
     CKH(hipEventRecord(e0, 0));
-    if (idf_rans_decode_streams(nullptr, S, doff, dwoff, dnw, dw, dm, ds, dfin, dfin2, dout, dst2)) return 1;
+    if (idf_rans_decode_streams(nullptr, S, n, doff, dwoff, dnw, dw, dm, ds, dfin, dfin2, dout, dst2, dws,
+                                idf_rans_decode_workspace_bytes(n))) return 1;
     CKH(hipEventRecord(e1, 0));
     CKH(hipEventSynchronize(e1));
     CKH(hipEventElapsedTime(&ms, e0, e1));
