@@ -1,0 +1,457 @@
+// vq_kernels.hip -- the VQ-VAE of the residual configs (configs 3-5; vqvae.py:22-168,
+// roundlib.py:41-89, extenddim.py:40-67) on gfx950.
+//
+// Activations are pixel-major ("NHWC") like the flow engine.  Every convolution of the
+// VQ-VAE -- Conv2d 4x4/s2/p1 and 3x3/p1 and 1x1 (VQEncoder), the ResBlock convs
+// (nnblock.py:59-84), and ConvTranspose2d 4x4/s2/p1 (VQDecoder) -- is one implicit GEMM
+// over a TAP TABLE: an output pixel on a "compute grid" (m, n) reads input pixels
+// (m*isy + dy[t], n*isx + dx[t]) for each tap t, and is written to output pixel
+// (m*osy + oy0, n*osx + ox0).  A stride-2 transposed conv is four such launches, one per
+// output parity class (each a 2x2-tap conv), so no zero-stuffed input is ever read.
+// K is ordered channel-slab-major, tap-minor (a slab's taps re-read the same lines from
+// L1/L2), the reduction order depends only on the weights' shape, and the epilogue fuses
+// bias, an optional residual add (ResBlock: act(x + conv)) and the activation.
+//
+// The vector quantiser (roundlib.py:56-62) is one fused kernel: a block keeps 64 latent
+// rows resident in LDS, streams the codebook through MFMA tiles and keeps a running
+// (distance, index) minimum per row -- the [rows x 16384] distance matrix never exists.
+// Distances are formed as the reference does, d = (|x|^2 + |e|^2) - 2 x.e in fp32, and
+// ties go to the lowest index (torch.argmin).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "idf_codec_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace idf {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int kMaxTaps = 16;
+
+struct ConvTapsArgs {
+  const float* X;
+  int64_t ldx;
+  int32_t B, Hi, Wi, C;
+  int32_t Hc, Wc;  // compute grid per image
+  int32_t isy, isx;
+  int32_t ntaps;
+  int32_t dy[kMaxTaps], dx[kMaxTaps];
+  const float* W;  // [n_alloc][ntaps][ldw]
+  int32_t ldw;
+  const float* bias;
+  int32_t N;
+  float* out;
+  int64_t ldo;
+  int32_t Ho, Wo, osy, osx, oy0, ox0;
+  const float* res;  // optional, indexed like out
+  int64_t ldr;
+  int32_t act;
+  float slope;
+  int64_t P;  // B * Hc * Wc
+  int32_t m_tiles, n_tiles;
+};
+
+__device__ __forceinline__ float vq_act(float v, int act, float slope) {
+  if (act == IDF_ACT_RELU) return v > 0.0f ? v : 0.0f;
+  if (act == IDF_ACT_LEAKY) return v > 0.0f ? v : v * slope;
+  if (act == IDF_ACT_TANH) return tanhf(v);
+  return v;
+}
+
+template <int BM, int BN, int WAVES_M, int WAVES_N>
+__global__ void __launch_bounds__(256) conv_taps_kernel(ConvTapsArgs g) {
+  constexpr int BK = 16;
+  constexpr int LDS_LD = BK + 8;  // conflict-free b128 fragment reads
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  constexpr int A_PER_T = BM * 4 / 256;
+  constexpr int B_F4 = BN * 4;
+  constexpr int B_PER_T = (B_F4 + 255) / 256;
+  static_assert(WAVES_M * WAVES_N == 4 && FM >= 1 && FN >= 1, "tile");
+
+  __shared__ __attribute__((aligned(16))) float As[2][BM][LDS_LD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN][LDS_LD];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int mt = blockIdx.x / g.n_tiles, nt = blockIdx.x % g.n_tiles;
+  const int64_t m0 = (int64_t)mt * BM;
+  const int n0 = nt * BN;
+  const int64_t hwc = (int64_t)g.Hc * g.Wc;
+
+  int a_row[A_PER_T], a_kq[A_PER_T], a_b[A_PER_T], a_m[A_PER_T], a_n[A_PER_T];
+  bool a_ok[A_PER_T];
+#pragma unroll
+  for (int j = 0; j < A_PER_T; ++j) {
+    const int f = tid + 256 * j;
+    a_row[j] = f >> 2;
+    a_kq[j] = f & 3;
+    const int64_t p = m0 + a_row[j];
+    a_ok[j] = p < g.P;
+    const int64_t pp = a_ok[j] ? p : 0;
+    a_b[j] = (int)(pp / hwc);
+    const int64_t rem = pp - (int64_t)a_b[j] * hwc;
+    a_m[j] = (int)(rem / g.Wc);
+    a_n[j] = (int)(rem - (int64_t)a_m[j] * g.Wc);
+  }
+  const int nslab = (g.C + BK - 1) / BK;
+  const int nk = nslab * g.ntaps;
+  f4 ra[A_PER_T], rb[B_PER_T];
+
+  auto load_chunk = [&](int kc) {
+    const int slab = kc / g.ntaps, tap = kc - slab * g.ntaps, c0 = slab * BK;
+    const int dy = g.dy[tap], dx = g.dx[tap];
+#pragma unroll
+    for (int j = 0; j < A_PER_T; ++j) {
+      const int c = c0 + 4 * a_kq[j];
+      const int iy = a_m[j] * g.isy + dy, ix = a_n[j] * g.isx + dx;
+      const bool ok = a_ok[j] && c < g.C && iy >= 0 && iy < g.Hi && ix >= 0 && ix < g.Wi;
+      ra[j] = ok ? *(const f4*)(g.X + (((int64_t)a_b[j] * g.Hi + iy) * g.Wi + ix) * g.ldx + c)
+                 : f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < B_PER_T; ++j) {
+      const int f = tid + 256 * j;
+      if (f < B_F4) {
+        const int n = f >> 2, kq = f & 3;
+        rb[j] = *(const f4*)(g.W + ((int64_t)(n0 + n) * g.ntaps + tap) * g.ldw + c0 + 4 * kq);
+      }
+    }
+  };
+  auto store_chunk = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < A_PER_T; ++j) *(f4*)&As[buf][a_row[j]][4 * a_kq[j]] = ra[j];
+#pragma unroll
+    for (int j = 0; j < B_PER_T; ++j) {
+      const int f = tid + 256 * j;
+      if (f < B_F4) *(f4*)&Bs[buf][f >> 2][4 * (f & 3)] = rb[j];
+    }
+  };
+
+  f4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  load_chunk(0);
+  store_chunk(0);
+  __syncthreads();
+  const int lr = lane & 15, lk = 4 * (lane >> 4);
+  for (int kc = 0; kc < nk; ++kc) {
+    const int buf = kc & 1;
+    if (kc + 1 < nk) load_chunk(kc + 1);
+    f4 fa[FM], fb[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) fa[i] = *(const f4*)&As[buf][wm * WTM + i * 16 + lr][lk];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) fb[j] = *(const f4*)&Bs[buf][wn * WTN + j * 16 + lr][lk];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][t], fb[j][t], acc[i][j], 0, 0, 0);
+    if (kc + 1 < nk) store_chunk(buf ^ 1);
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wn * WTN + j * 16 + lr;
+    if (n >= g.N) continue;
+    const float bv = g.bias ? g.bias[n] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t p = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+        if (p >= g.P) continue;
+        const int64_t b = p / hwc, rem = p - b * hwc;
+        const int m = (int)(rem / g.Wc), nn = (int)(rem - (int64_t)m * g.Wc);
+        const int64_t o = (b * g.Ho + (int64_t)m * g.osy + g.oy0) * g.Wo + (int64_t)nn * g.osx + g.ox0;
+        float v = acc[i][j][r] + bv;
+        if (g.res) v = g.res[o * g.ldr + n] + v;  // ResBlock: x + resblock(x) (nnblock.py:81-82)
+        g.out[o * g.ldo + n] = vq_act(v, g.act, g.slope);
+      }
+  }
+}
+
+template <int BN>
+static int launch_taps(ConvTapsArgs a, hipStream_t s) {
+  constexpr int WN = BN >= 64 ? 2 : 1;
+  constexpr int WM = 4 / WN;
+  constexpr int BM = 64;
+  a.m_tiles = (int)((a.P + BM - 1) / BM);
+  a.n_tiles = (a.N + BN - 1) / BN;
+  hipLaunchKernelGGL((conv_taps_kernel<BM, BN, WM, WN>), dim3((unsigned)(a.m_tiles * a.n_tiles)),
+                     dim3(256), 0, s, a);
+  return idf_last_error();
+}
+
+// ---------------------------------------------------------------- vector quantiser
+// rows [P][ldx] (D columns), codebook E [K][lde], enorm[k] = |e_k|^2 (fp32, sum in index
+// order).  idx[p] = argmin_k ((|x|^2 + enorm[k]) - 2 x.e_k), lowest k on ties.
+constexpr int kVqBM = 64, kVqBN = 64, kVqMaxD = 512;
+
+__global__ void __launch_bounds__(256) vq_argmin_kernel(int64_t P, int32_t D, const float* __restrict__ X,
+                                                        int64_t ldx, const float* __restrict__ E,
+                                                        int32_t lde, int32_t K,
+                                                        const float* __restrict__ enorm,
+                                                        int32_t* __restrict__ idx) {
+  constexpr int APITCH = kVqMaxD + 4;  // rows 4 dwords apart: conflict-free fragment reads
+  constexpr int BK = 16, BLD = BK + 8;
+  __shared__ __attribute__((aligned(16))) float As[kVqBM * APITCH];
+  __shared__ __attribute__((aligned(16))) float Bs[2][kVqBN][BLD];
+  __shared__ float x2s[kVqBM];
+  __shared__ float bestv[4][kVqBM];
+  __shared__ int besti[4][kVqBM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t m0 = (int64_t)blockIdx.x * kVqBM;
+  // stage the block's rows (zero beyond P / D)
+  const int dq = (D + 3) / 4;
+  for (int f = tid; f < kVqBM * (kVqMaxD / 4); f += 256) {
+    const int r = f / (kVqMaxD / 4), q = f - r * (kVqMaxD / 4);
+    const int64_t p = m0 + r;
+    f4 v = f4{0.f, 0.f, 0.f, 0.f};
+    if (p < P && q < dq) v = *(const f4*)(X + p * ldx + 4 * q);
+    *(f4*)&As[r * APITCH + 4 * q] = v;
+  }
+  __syncthreads();
+  if (tid < kVqBM) {  // |x|^2 in index order
+    float s = 0.0f;
+    for (int c = 0; c < D; ++c) s = __builtin_fmaf(As[tid * APITCH + c], As[tid * APITCH + c], s);
+    x2s[tid] = s;
+  }
+  // each wave: 16 rows (wave) x 64 codes per tile (4 n-fragments)
+  const int lr = lane & 15, lk = 4 * (lane >> 4);
+  const int nkc = (D + BK - 1) / BK;
+  float best[4];
+  int bidx[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    best[r] = __builtin_inff();
+    bidx[r] = 0x7fffffff;
+  }
+  f4 rb;
+  auto load_b = [&](int k0, int kc) {
+    const int n = tid >> 2, q = tid & 3;
+    const int c = kc * BK + 4 * q;
+    rb = (k0 + n < K && c < D) ? *(const f4*)(E + (int64_t)(k0 + n) * lde + c) : f4{0.f, 0.f, 0.f, 0.f};
+  };
+  __syncthreads();
+  for (int k0 = 0; k0 < K; k0 += kVqBN) {
+    f4 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = f4{0.f, 0.f, 0.f, 0.f};
+    load_b(k0, 0);
+    *(f4*)&Bs[0][tid >> 2][4 * (tid & 3)] = rb;
+    __syncthreads();
+    for (int kc = 0; kc < nkc; ++kc) {
+      const int buf = kc & 1;
+      if (kc + 1 < nkc) load_b(k0, kc + 1);
+      const f4 fa = *(const f4*)&As[(wave * 16 + lr) * APITCH + kc * BK + lk];
+      f4 fb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = *(const f4*)&Bs[buf][j * 16 + lr][lk];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[t], fb[j][t], acc[j], 0, 0, 0);
+      if (kc + 1 < nkc) *(f4*)&Bs[buf ^ 1][tid >> 2][4 * (tid & 3)] = rb;
+      __syncthreads();
+    }
+    // lane holds rows wave*16 + (lane>>4)*4 + r, code k0 + j*16 + (lane&15)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + j * 16 + lr;
+      if (k >= K) continue;
+      const float en = enorm[k];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float x2 = x2s[wave * 16 + (lane >> 4) * 4 + r];
+        const float d = (x2 + en) - 2.0f * acc[j][r];
+        if (d < best[r] || (d == best[r] && k < bidx[r])) {
+          best[r] = d;
+          bidx[r] = k;
+        }
+      }
+    }
+  }
+  // reduce over the 16 lanes sharing each row (lanes differ in code column)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const float ov = __shfl_xor(best[r], o);
+      const int oi = __shfl_xor(bidx[r], o);
+      if (ov < best[r] || (ov == best[r] && oi < bidx[r])) {
+        best[r] = ov;
+        bidx[r] = oi;
+      }
+    }
+  }
+  if (lr == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = wave * 16 + (lane >> 4) * 4 + r;
+      const int64_t p = m0 + row;
+      if (p < P) idx[p] = bidx[r];
+    }
+  }
+}
+
+// |e_k|^2 in index order (the reference's torch.sum(weight**2, dim=1) up to summation order)
+__global__ void vq_norms_kernel(int32_t K, int32_t D, const float* __restrict__ E, int32_t lde,
+                                float* __restrict__ enorm) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  float s = 0.0f;
+  for (int c = 0; c < D; ++c) s = __builtin_fmaf(E[(int64_t)k * lde + c], E[(int64_t)k * lde + c], s);
+  enorm[k] = s;
+}
+
+// out[p, c] = E[idx[p], c] (nn.Embedding lookup, vqvae.py:58 / roundlib.py:63)
+__global__ void vq_gather_kernel(int64_t P, int32_t D, const int32_t* __restrict__ idx,
+                                 const float* __restrict__ E, int32_t lde, float* __restrict__ out,
+                                 int64_t ldo) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P * D) return;
+  const int64_t p = i / D;
+  const int c = (int)(i - p * D);
+  out[p * ldo + c] = E[(int64_t)idx[p] * lde + c];
+}
+
+// y[p, c] = op(x[p, c]) on pixel-major buffers:
+// 0: (x - 0.5) / 0.5            (trainer.py:606 input scaling)
+// 1: rint((x * 0.5 + 0.5) * 256) / 256   (trainer.py:606-607: rescale + model.round)
+// 2: x - z                      (trainer.py:608: res = data - rec)
+// 3: x + z                      (decode: data = res + rec)
+__global__ void vq_pointwise_kernel(int64_t P, int32_t C, int32_t op, const float* __restrict__ x,
+                                    int64_t ldx, const float* __restrict__ z, int64_t ldz,
+                                    float* __restrict__ y, int64_t ldy) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P * C) return;
+  const int64_t p = i / C;
+  const int c = (int)(i - p * C);
+  const float v = x[p * ldx + c];
+  float r;
+  if (op == 0) r = (v - 0.5f) / 0.5f;
+  else if (op == 1) r = __builtin_rintf((v * 0.5f + 0.5f) * 256.0f) / 256.0f;
+  else if (op == 2) r = v - z[p * ldz + c];
+  else r = v + z[p * ldz + c];
+  y[p * ldy + c] = r;
+}
+
+// Patching.forward (extenddim.py:52-58) on NCHW: [B, C, H, W] -> [B*(H/h)*(W/w), C, h, w];
+// inverse = backward (extenddim.py:60-67).
+__global__ void patch_kernel(int32_t B, int32_t C, int32_t H, int32_t W, int32_t h, int32_t w,
+                             int32_t inverse, const float* __restrict__ src, float* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)B * C * H * W;
+  if (i >= total) return;
+  // i indexes the image layout [B][C][H][W]
+  const int x = (int)(i % W);
+  int64_t t = i / W;
+  const int y = (int)(t % H);
+  t /= H;
+  const int c = (int)(t % C);
+  const int64_t b = t / C;
+  const int hh = H / h, ww = W / w;
+  const int64_t q = (b * hh + y / h) * ww + x / w;  // patch index
+  const int64_t j = ((q * C + c) * h + (y % h)) * w + (x % w);
+  if (inverse) dst[i] = src[j];
+  else dst[j] = src[i];
+}
+
+}  // namespace idf
+
+using namespace idf;
+
+extern "C" {
+
+int idf_conv_taps_f32(void* stream, int32_t B, int32_t Hi, int32_t Wi, int32_t C, const float* x,
+                      int64_t ld_x, int32_t Hc, int32_t Wc, int32_t isy, int32_t isx, int32_t ntaps,
+                      const int32_t* dy, const int32_t* dx, const float* w, int32_t ldw,
+                      int32_t n_alloc, const float* bias, int32_t N, float* out, int64_t ld_out,
+                      int32_t Ho, int32_t Wo, int32_t osy, int32_t osx, int32_t oy0, int32_t ox0,
+                      const float* res, int64_t ld_res, int32_t act, float slope) {
+  if (B <= 0 || Hc <= 0 || Wc <= 0 || N <= 0) return IDF_OK;
+  if (ntaps < 1 || ntaps > kMaxTaps || C <= 0 || (C & 3) || (ld_x & 3) || (ldw & 15) ||
+      ldw < ((C + 15) / 16) * 16 || !dy || !dx)
+    return IDF_ERR_ARG;
+  ConvTapsArgs a = {};
+  a.X = x; a.ldx = ld_x; a.B = B; a.Hi = Hi; a.Wi = Wi; a.C = C; a.Hc = Hc; a.Wc = Wc;
+  a.isy = isy; a.isx = isx; a.ntaps = ntaps;
+  for (int t = 0; t < ntaps; ++t) {
+    a.dy[t] = dy[t];
+    a.dx[t] = dx[t];
+  }
+  a.W = w; a.ldw = ldw; a.bias = bias; a.N = N; a.out = out; a.ldo = ld_out;
+  a.Ho = Ho; a.Wo = Wo; a.osy = osy; a.osx = osx; a.oy0 = oy0; a.ox0 = ox0;
+  a.res = res; a.ldr = ld_res; a.act = act; a.slope = slope;
+  a.P = (int64_t)B * Hc * Wc;
+  const int bn = N <= 32 ? 32 : (N <= 64 ? 64 : 128);
+  if (n_alloc < ((N + bn - 1) / bn) * bn) return IDF_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (bn == 32) return launch_taps<32>(a, s);
+  if (bn == 64) return launch_taps<64>(a, s);
+  return launch_taps<128>(a, s);
+}
+
+int idf_conv_taps_n_alloc(int32_t N) {
+  const int bn = N <= 32 ? 32 : (N <= 64 ? 64 : 128);
+  return ((N + bn - 1) / bn) * bn;
+}
+
+int idf_vq_norms(void* stream, int32_t K, int32_t D, const float* e, int32_t lde, float* enorm) {
+  if (K <= 0) return IDF_OK;
+  hipLaunchKernelGGL(vq_norms_kernel, dim3((K + 255) / 256), dim3(256), 0, (hipStream_t)stream, K, D,
+                     e, lde, enorm);
+  return idf_last_error();
+}
+
+int idf_vq_argmin(void* stream, int64_t P, int32_t D, const float* x, int64_t ld_x, const float* e,
+                  int32_t lde, int32_t K, const float* enorm, int32_t* idx) {
+  if (P <= 0) return IDF_OK;
+  if (D <= 0 || D > kVqMaxD || (D & 3) || (ld_x & 3) || (lde & 3) || K <= 0) return IDF_ERR_ARG;
+  hipLaunchKernelGGL(vq_argmin_kernel, dim3((unsigned)((P + kVqBM - 1) / kVqBM)), dim3(256), 0,
+                     (hipStream_t)stream, P, D, x, ld_x, e, lde, K, enorm, idx);
+  return idf_last_error();
+}
+
+int idf_vq_gather(void* stream, int64_t P, int32_t D, const int32_t* idx, const float* e,
+                  int32_t lde, float* out, int64_t ld_out) {
+  const int64_t n = P * D;
+  if (n <= 0) return IDF_OK;
+  hipLaunchKernelGGL(vq_gather_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, P, D, idx, e, lde, out, ld_out);
+  return idf_last_error();
+}
+
+int idf_vq_pointwise(void* stream, int64_t P, int32_t C, int32_t op, const float* x, int64_t ld_x,
+                     const float* z, int64_t ld_z, float* y, int64_t ld_y) {
+  const int64_t n = P * C;
+  if (n <= 0) return IDF_OK;
+  if (op < 0 || op > 3 || (op >= 2 && !z)) return IDF_ERR_ARG;
+  hipLaunchKernelGGL(vq_pointwise_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, P, C, op, x, ld_x, z, ld_z, y, ld_y);
+  return idf_last_error();
+}
+
+int idf_patch(void* stream, int32_t B, int32_t C, int32_t H, int32_t W, int32_t h, int32_t w,
+              int32_t inverse, const float* src, float* dst) {
+  if (h <= 0 || w <= 0 || H % h || W % w) return IDF_ERR_ARG;
+  const int64_t n = (int64_t)B * C * H * W;
+  if (n <= 0) return IDF_OK;
+  hipLaunchKernelGGL(patch_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, B, C, H, W, h, w, inverse, src, dst);
+  return idf_last_error();
+}
+
+}  // extern "C"

@@ -2,7 +2,8 @@
 theoretical bpd the reference logs next to the real one (flows.py:154-169);
 it is not on the coding path (the coder uses the bit-exact CDF of
 idfcodec/csrc/idf_cdf.h).  BinomialDistribution / UnitGaussianDistribution are
-VQ-VAE training losses and out of scope."""
+VQ-VAE training losses (distlib.py:73-101); they are registered so the residual
+configs construct, and compute with torch.distributions (not a coding path)."""
 import torch
 import torch.nn.functional as F
 from torch import nn
@@ -45,3 +46,25 @@ class DLogistic(Distribution):
         u = torch.rand_like(mean)
         s = torch.log(u / (1 - u)) * torch.exp(logscale) + mean
         return self.round(s, nbits=nbits)
+
+
+@NNDistribution.register
+class BinomialDistribution(nn.Module):
+    """distlib.py:73-90 (VQ-VAE training loss only)."""
+
+    def log_prob(self, x, y):
+        return torch.distributions.Binomial(255, y).log_prob(torch.round(x * 255))
+
+    def sample(self, y):
+        pass
+
+
+@NNDistribution.register
+class UnitGaussianDistribution(nn.Module):
+    """distlib.py:93-101 (VQ-VAE training loss only)."""
+
+    def log_prob(self, x, y):
+        return torch.distributions.Normal(y, torch.ones_like(y)).log_prob(x)
+
+    def sample(self, y):
+        pass

@@ -105,6 +105,15 @@ SIGNATURES = {
     "idf_pm_to_nchw": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P]),
     "idf_nchw_to_pm": (ctypes.c_int, [P, i32, i32, i32, i32, P, P, i64]),
     "idf_conv4x4s2_f32": (ctypes.c_int, [P, i32, i32, i32, i32, i32, P, i64, P, P, P, i64]),
+    "idf_conv_taps_n_alloc": (ctypes.c_int, [i32]),
+    "idf_conv_taps_f32": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, i32, i32, i32, i32, i32, P,
+                                         P, P, i32, i32, P, i32, P, i64, i32, i32, i32, i32, i32,
+                                         i32, P, i64, i32, f32]),
+    "idf_vq_norms": (ctypes.c_int, [P, i32, i32, P, i32, P]),
+    "idf_vq_argmin": (ctypes.c_int, [P, i64, i32, P, i64, P, i32, i32, P, P]),
+    "idf_vq_gather": (ctypes.c_int, [P, i64, i32, P, P, i32, P, i64]),
+    "idf_vq_pointwise": (ctypes.c_int, [P, i64, i32, i32, P, i64, P, i64, P, i64]),
+    "idf_patch": (ctypes.c_int, [P, i32, i32, i32, i32, i32, i32, i32, P, P]),
 }
 
 _lib = None

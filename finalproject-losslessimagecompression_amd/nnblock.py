@@ -3,8 +3,9 @@ channels by growth_channel in total, then a zero-initialised 1x1 head.  On the
 device the whole block is ONE call into libidfcodec (idf_dense_block_f32): the
 concatenations are column ranges of one pixel-major feature buffer.
 
-ResBlock (nnblock.py:59-84) is the VQ-VAE's block (configs 3-5, SURVEY 8(f)
-rank 1) and is not part of this round."""
+ResBlock (nnblock.py:59-84) is the VQ-VAE's residual block (configs 3-5); on the
+device it runs inside idfcodec.vq.VQEngine as two tap-table convs, the second
+with the residual add and ReLU fused into its epilogue."""
 from copy import deepcopy
 
 from torch import nn
@@ -44,3 +45,26 @@ class DenseBlock(nn.Module):
     def forward(self, x):
         from idfcodec.modules import run_dense_block
         return run_dense_block(self, x)
+
+
+@NNBlock.register
+class ResBlock(nn.Module):
+    """nnblock.py:59-84: relu(x + conv3x3(relu(conv3x3(x))))."""
+
+    def __init__(self, channel: int, batch_norm: bool = False):
+        super().__init__()
+        self.channel = channel
+        if batch_norm:
+            self.resblock = nn.Sequential(
+                nn.Conv2d(channel, channel, kernel_size=3, padding=1), nn.ReLU(True),
+                nn.BatchNorm2d(channel),
+                nn.Conv2d(channel, channel, kernel_size=3, padding=1), nn.BatchNorm2d(channel))
+        else:
+            self.resblock = nn.Sequential(
+                nn.Conv2d(channel, channel, kernel_size=3, padding=1), nn.ReLU(True),
+                nn.Conv2d(channel, channel, kernel_size=3, padding=1))
+        self.act = nn.ReLU(True)
+
+    def forward(self, x):
+        raise NotImplementedError("ResBlock runs inside the VQ-VAE engine (idfcodec.vq); "
+                                  "call VQVAE.forward / encode / decode")

@@ -291,6 +291,39 @@ int idf_conv4x4s2_f32(void *stream, int32_t B, int32_t H, int32_t W, int32_t ci,
                       const float *d_src, int64_t ld_src, const float *d_w, const float *d_bias,
                       float *d_dst, int64_t ld_dst);
 
+/* ======================================================================== *
+ * VQ-VAE of the residual configs (vqvae.py:22-168; configs 3-5), pixel-major fp32.
+ * ======================================================================== */
+/* Implicit-GEMM convolution over a tap table: for every compute-grid pixel (b, m, n),
+ * m < Hc, n < Wc:  v[c_out] = bias + sum_{t < ntaps, c < C} X[b, m*isy+dy[t], n*isx+dx[t], c]
+ * * W[c_out][t][c] (out-of-image taps read 0); out pixel (b, m*osy+oy0, n*osx+ox0) of an
+ * Ho x Wo image gets act(v) or, with d_res, act(res[same pixel] + v) (ResBlock,
+ * nnblock.py:80-84).  W: [n_alloc][ntaps][ldw], n_alloc = idf_conv_taps_n_alloc(N),
+ * ldw >= C rounded to 16, zero-padded.  Conv2d(k, s, p): Hc = Ho, isy = s, taps
+ * (ky - p, kx - p); ConvTranspose2d(4, 2, 1): four launches, one per output parity. */
+int idf_conv_taps_n_alloc(int32_t N);
+int idf_conv_taps_f32(void *stream, int32_t B, int32_t Hi, int32_t Wi, int32_t C, const float *d_x,
+                      int64_t ld_x, int32_t Hc, int32_t Wc, int32_t isy, int32_t isx, int32_t ntaps,
+                      const int32_t *dy, const int32_t *dx, const float *d_w, int32_t ldw,
+                      int32_t n_alloc, const float *d_bias, int32_t N, float *d_out, int64_t ld_out,
+                      int32_t Ho, int32_t Wo, int32_t osy, int32_t osx, int32_t oy0, int32_t ox0,
+                      const float *d_res, int64_t ld_res, int32_t act, float slope);
+/* VectorQuantizer.forward's index (roundlib.py:56-62): enorm[k] = |e_k|^2, then
+ * idx[p] = argmin_k ((|x_p|^2 + enorm[k]) - 2 x_p.e_k), lowest k on ties; D <= 512. */
+int idf_vq_norms(void *stream, int32_t K, int32_t D, const float *d_e, int32_t lde, float *d_enorm);
+int idf_vq_argmin(void *stream, int64_t P, int32_t D, const float *d_x, int64_t ld_x,
+                  const float *d_e, int32_t lde, int32_t K, const float *d_enorm, int32_t *d_idx);
+/* nn.Embedding lookup: out[p, c] = e[idx[p], c], c < D. */
+int idf_vq_gather(void *stream, int64_t P, int32_t D, const int32_t *d_idx, const float *d_e,
+                  int32_t lde, float *d_out, int64_t ld_out);
+/* y = op(x[, z]) elementwise on [P][C] pixel-major: 0 (x-0.5)/0.5, 1 rint((x*0.5+0.5)*256)/256,
+ * 2 x - z, 3 x + z (trainer.py:606-608 residual split and its inverse). */
+int idf_vq_pointwise(void *stream, int64_t P, int32_t C, int32_t op, const float *d_x, int64_t ld_x,
+                     const float *d_z, int64_t ld_z, float *d_y, int64_t ld_y);
+/* Patching.forward / backward (extenddim.py:52-67) on NCHW: [B,C,H,W] <-> [B*(H/h)*(W/w),C,h,w]. */
+int idf_patch(void *stream, int32_t B, int32_t C, int32_t H, int32_t W, int32_t h, int32_t w,
+              int32_t inverse, const float *d_src, float *d_dst);
+
 #ifdef __cplusplus
 }
 #endif
