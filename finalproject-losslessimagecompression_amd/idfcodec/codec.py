@@ -195,7 +195,26 @@ class ImageCodec:
         return self.coder.encode(ws, B, compact=compact)
 
     @torch.no_grad()
-    def decode(self, bs: Bitstream, cond=None, verify: bool = True):
+    def encode_nchw(self, x: torch.Tensor, cond=None, compact: bool = True) -> Bitstream:
+        """float NCHW input on the 1/256 grid (e.g. the residual data - rec of the residual
+        configs, trainer.py:608) -> Bitstream."""
+        _lib.require_device(x, "flow input")
+        B = x.shape[0]
+        ws = self.engine.load_nchw(x.float().contiguous())
+        self.engine.forward_pm(B, cond=cond)
+        return self.coder.encode(ws, B, compact=compact)
+
+    @torch.no_grad()
+    def decode_nchw(self, bs: Bitstream, cond=None, verify: bool = True):
+        """inverse of encode_nchw -> (float NCHW, info)."""
+        ws, info = self._decode_ws(bs, cond)
+        x = self.engine.image_nchw(ws, bs.n_images)
+        if verify:
+            info["ok"] = bool((info["final_states"] == RANS_L).all().item()) and not bool(
+                (info["status"] & ~_lib.STREAM_WORDS_LEFT).any().item())
+        return x, info
+
+    def _decode_ws(self, bs: Bitstream, cond):
         eng = self.engine
         dev = eng.device
         B = bs.n_images
@@ -214,9 +233,14 @@ class ImageCodec:
             self.coder.decode_level(bs, B, l, ws, word_off, out_state, out_status)
 
         ws = eng.inverse_pm(B, dec, cond=cond)
-        img, bad = eng.image_u8(ws, B)
-        info = {"final_states": out_state, "status": out_status, "off_grid": bad}
+        return ws, {"final_states": out_state, "status": out_status}
+
+    @torch.no_grad()
+    def decode(self, bs: Bitstream, cond=None, verify: bool = True):
+        ws, info = self._decode_ws(bs, cond)
+        img, bad = self.engine.image_u8(ws, bs.n_images)
+        info["off_grid"] = bad
         if verify:
-            ok = bool((out_state == RANS_L).all().item()) and int(bad.item()) == 0
-            info["ok"] = ok and not bool((out_status & ~_lib.STREAM_WORDS_LEFT).any().item())
+            ok = bool((info["final_states"] == RANS_L).all().item()) and int(bad.item()) == 0
+            info["ok"] = ok and not bool((info["status"] & ~_lib.STREAM_WORDS_LEFT).any().item())
         return img, info

@@ -41,8 +41,36 @@ CONFIGS = {
 }
 
 
+def _vqvae(embed_num, embed_dim, hidden, block_num=8):
+    blk = {"name": "ResBlock", "batch_norm": False}
+    return {"name": "VQVAE", "channel": 3, "embed_num": embed_num, "embed_dim": embed_dim,
+            "encoder": {"name": "VQEncoder", "block_num": block_num, "block": dict(blk)},
+            "decoder": {"name": "VQDecoder", "block_num": block_num, "block": dict(blk)},
+            "distribution": {"name": "BinomialDistribution"},
+            "vectorquantizer": {"reinit_interval": 1000, "threshold": 0.1},
+            "hidden_dims": list(hidden), "batch_norm": False}
+
+
+# VQ-VAE sections and input sizes of the residual configs (ResidualTrainer; the
+# checkpoints they name are absent, so the weights are the seeded initialisation)
+VQVAE = {
+    # configs/resflow-cond-imagenet64.yaml:46-73, input_size :75-77
+    "resflow-cond-imagenet64": (_vqvae(16384, 512, [128, 256, 384]), (64, 64)),
+    # configs/resflows_smallpatch_split.yaml:44-75 (BASELINE configs[3]: synthetic 256x256)
+    "resflows_smallpatch_split": (_vqvae(8192, 512, [128, 256, 512]), (256, 256)),
+    # configs/resflow-patches-vqvae.yaml:46-78 (215x178 CelebA padded to 216x184)
+    "resflow-patches-vqvae": (_vqvae(8192, 512, [128, 256, 512]), (216, 184)),
+}
+
+
 def get(name: str) -> dict:
     return copy.deepcopy(CONFIGS[name])
+
+
+def get_vqvae(name: str):
+    """(VQVAE kwargs incl. name, input_size) of a residual config."""
+    cfg, size = VQVAE[name]
+    return copy.deepcopy(cfg), tuple(size)
 
 
 def load_yaml(path: str) -> dict:

@@ -1,0 +1,166 @@
+"""Lossless codec of the residual configs (configs 3-5; trainer.py:550-801 ResidualTrainer).
+
+encode (trainer.py:603-621, made lossless):
+  u8 -> data on the 1/256 grid (trainer.py:101) -> VQ-VAE indices (vqvae.py:135-147) ->
+  rec = round8(decoder(embed[idx]) * 0.5 + 0.5) (trainer.py:606-607) -> res = data - rec
+  (:608) -> Patching (extenddim.py:52-58) of res and rec -> the flow model's forward with
+  cond = rec patches (ConditionalFlows) -> rANS streams.
+  The VQ indices travel too, as a fixed-width code of ceil(log2(embed_num)) bits each --
+  the reference counts only the residual's bits (trainer.py:698-701) and never codes the
+  indices; bits() reports both parts.
+decode: indices -> rec (the same device function as the encoder side) -> flow decode with
+  cond = rec patches -> unpatch -> data = res + rec -> uint8 (exact on the grid).
+"""
+from __future__ import annotations
+
+import math
+import struct
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr
+from .codec import Bitstream, ImageCodec
+
+MAGIC = b"IDFR"
+VERSION = 1
+
+
+@dataclass
+class ResidualBitstream:
+    flow: Bitstream
+    idx_words: torch.Tensor     # int32 view of the packed index words
+    n_images: int
+    image_shape: tuple          # (C, H, W)
+    grid: tuple                 # (h, w) of the VQ indices per image
+    embed_num: int
+
+    @property
+    def index_bits(self) -> int:
+        return max(1, math.ceil(math.log2(self.embed_num)))
+
+    def bits(self) -> int:
+        """flow streams (the reference's accounting, trainer.py:326-327) + index code"""
+        return self.flow.bits() + self.n_images * self.grid[0] * self.grid[1] * self.index_bits
+
+    def bpd(self) -> float:
+        C, H, W = self.image_shape
+        return self.bits() / (self.n_images * C * H * W)
+
+    def to_bytes(self) -> bytes:
+        C, H, W = self.image_shape
+        hdr = struct.pack("<4sHHIIIIIII", MAGIC, VERSION, 0, self.n_images, C, H, W,
+                          self.grid[0], self.grid[1], self.embed_num)
+        iw = self.idx_words.detach().cpu().numpy().astype("<i4").tobytes()
+        fb = self.flow.to_bytes()
+        return hdr + struct.pack("<QQ", len(iw), len(fb)) + iw + fb
+
+    @classmethod
+    def from_bytes(cls, buf: bytes, device=None) -> "ResidualBitstream":
+        fmt = "<4sHHIIIIIII"
+        magic, ver, _f, n, C, H, W, h, w, K = struct.unpack_from(fmt, buf, 0)
+        if magic != MAGIC or ver != VERSION:
+            raise ValueError("not an IDF residual bitstream")
+        o = struct.calcsize(fmt)
+        li, lf = struct.unpack_from("<QQ", buf, o)
+        o += 16
+        iw = np.frombuffer(buf, "<i4", li // 4, o).copy()
+        o += li
+        flow = Bitstream.from_bytes(buf[o:o + lf], device)
+        t = torch.from_numpy(iw)
+        return cls(flow, t.to(device) if device else t, n, (C, H, W), (h, w), K)
+
+
+class ResidualCodec:
+    """uint8 images <-> ResidualBitstream with a flow model (ConditionalFlows or IDFlows)
+    over Patching(input_size -> model H x W) and a VQ-VAE."""
+
+    def __init__(self, flows_model, vqvae, input_size):
+        from extenddim import Patching
+        self.flows = flows_model
+        self.vqvae = vqvae
+        self.H, self.W = int(input_size[0]), int(input_size[1])
+        self.patch = Patching(self.H, self.W, flows_model.H, flows_model.W)
+        self.conditional = type(flows_model).__name__ == "ConditionalFlows"
+        self.bits = max(1, math.ceil(math.log2(vqvae.embed_num)))
+
+    def _codec(self) -> ImageCodec:
+        return self.flows.codec()
+
+    def _dequant(self, img_u8):
+        B, C, H, W = img_u8.shape
+        dev = img_u8.device
+        s = _lib.stream_ptr(dev)
+        pm = torch.empty(B * H * W * 4, dtype=torch.float32, device=dev)
+        check(lib().idf_dequant_u8(s, B, C, H, W, ptr(img_u8), ptr(pm), 4), "dequant")
+        out = torch.empty((B, C, H, W), dtype=torch.float32, device=dev)
+        check(lib().idf_pm_to_nchw(s, B, C, H, W, ptr(pm), 4, ptr(out)), "pm->nchw")
+        return out
+
+    @staticmethod
+    def _pointwise(op, x, z):
+        out = torch.empty_like(x)
+        n = x.numel()
+        check(lib().idf_vq_pointwise(_lib.stream_ptr(x.device), n, 1, op, ptr(x), 1, ptr(z), 1,
+                                     ptr(out), 1), "pointwise")
+        return out
+
+    @torch.no_grad()
+    def encode(self, img_u8: torch.Tensor) -> ResidualBitstream:
+        _lib.require_device(img_u8, "image batch")
+        if img_u8.dtype != torch.uint8:
+            raise TypeError("ResidualCodec.encode expects uint8 images")
+        img_u8 = img_u8.contiguous()
+        B, C, H, W = img_u8.shape
+        assert (H, W) == (self.H, self.W), (H, W)
+        data = self._dequant(img_u8)
+        idx = self.vqvae.indices(data)                       # [B, h, w] int32
+        rec = self.vqvae.reconstruct(idx)                    # NCHW on the grid
+        res = self._pointwise(2, data, rec)                  # data - rec
+        res_p, _ = self.patch.forward(res, None)
+        codec = self._codec()
+        if self.conditional:
+            rec_p, _ = self.patch.forward(rec, None)
+            flow = codec.encode_nchw(res_p, cond=rec_p.contiguous())
+        else:
+            flow = codec.encode_nchw(res_p)
+        n = idx.numel()
+        words = torch.empty(max(int(lib().idf_pack_bits_words(n, self.bits)), 1),
+                            dtype=torch.int32, device=img_u8.device)
+        check(lib().idf_pack_bits(_lib.stream_ptr(img_u8.device), n, self.bits, ptr(idx),
+                                  ptr(words)), "pack idx")
+        return ResidualBitstream(flow, words, B, (C, H, W), tuple(idx.shape[1:]),
+                                 self.vqvae.embed_num)
+
+    @torch.no_grad()
+    def decode(self, rbs: ResidualBitstream, verify: bool = True):
+        dev = next(self.flows.parameters()).device
+        B = rbs.n_images
+        C, H, W = rbs.image_shape
+        h, w = rbs.grid
+        n = B * h * w
+        words = rbs.idx_words.to(dev)
+        idx = torch.empty(n, dtype=torch.int32, device=dev)
+        check(lib().idf_unpack_bits(_lib.stream_ptr(dev), n, self.bits, ptr(words), ptr(idx)),
+              "unpack idx")
+        rec = self.vqvae.reconstruct(idx.view(B, h, w))
+        codec = self._codec()
+        if self.conditional:
+            rec_p, _ = self.patch.forward(rec, None)
+            res_p, info = codec.decode_nchw(rbs.flow, cond=rec_p.contiguous(), verify=verify)
+        else:
+            res_p, info = codec.decode_nchw(rbs.flow, verify=verify)
+        res = self.patch.backward(res_p.contiguous())
+        data = self._pointwise(3, res, rec)                  # res + rec
+        s = _lib.stream_ptr(dev)
+        pm = torch.empty(B * H * W * 4, dtype=torch.float32, device=dev)
+        check(lib().idf_nchw_to_pm(s, B, C, H, W, ptr(data), ptr(pm), 4), "nchw->pm")
+        img = torch.empty((B, C, H, W), dtype=torch.uint8, device=dev)
+        bad = torch.zeros(1, dtype=torch.int32, device=dev)
+        check(lib().idf_quant_u8(s, B, C, H, W, ptr(pm), 4, ptr(img), ptr(bad)), "quant")
+        info["off_grid"] = bad
+        if verify:
+            info["ok"] = bool(info.get("ok", True)) and int(bad.item()) == 0
+        return img, info

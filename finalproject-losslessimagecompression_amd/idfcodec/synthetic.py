@@ -39,3 +39,23 @@ def build_model(cfg: dict, head_std: float = 0.05, seed: int = 0, head_seed: int
 def images(B: int, C: int = 3, H: int = 64, W: int = 64, seed: int = 2) -> torch.Tensor:
     g = torch.Generator().manual_seed(seed)
     return torch.randint(0, 256, (B, C, H, W), generator=g, dtype=torch.uint8)
+
+
+def build_vqvae(cfg: dict, seed: int = 0):
+    """The residual configs' VQ-VAE at its seeded initialisation (vqvae.py mirror)."""
+    import vqvae  # noqa: F401  (registers VQVAE / VQEncoder / VQDecoder)
+    cfg = copy.deepcopy(cfg)
+    random.seed(seed)
+    torch.manual_seed(seed)
+    from vqvae import EnDecoder
+    return EnDecoder.get(cfg.pop("name"))(**cfg).eval()
+
+
+def build_residual(name: str, device="cuda"):
+    """(ResidualCodec, flows model, vqvae, input_size) of a residual north-star config."""
+    from idfcodec import configs
+    from idfcodec.residual import ResidualCodec
+    vcfg, size = configs.get_vqvae(name)
+    flows_model = build_model(configs.get(name)).to(device)
+    vq = build_vqvae(vcfg).to(device)
+    return ResidualCodec(flows_model, vq, size), flows_model, vq, size
