@@ -370,25 +370,29 @@ __global__ void patch_kernel(int32_t B, int32_t C, int32_t H, int32_t W, int32_t
 }
 
 // Fixed-width index code (the VQ indices of the residual configs):
-// index i occupies bits [i*bits, (i+1)*bits) of the little-endian word stream.
-__global__ void pack_bits_kernel(int64_t n, int32_t bits, const int32_t* __restrict__ idx,
-                                 uint32_t* __restrict__ words) {
+// indices come in groups (one image each) of `per` indices; group g starts at word
+// g * wpg (wpg = ceil(per * bits / 32)), and its index j occupies bits
+// [j*bits, (j+1)*bits) of that little-endian word run -- so shards concatenate.
+__global__ void pack_bits_kernel(int64_t n, int64_t per, int64_t wpg, int32_t bits,
+                                 const int32_t* __restrict__ idx, uint32_t* __restrict__ words) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  const int64_t g = i / per, j = i - g * per;
   const uint64_t v = (uint64_t)(uint32_t)idx[i] & ((1ull << bits) - 1);
-  const uint64_t b0 = (uint64_t)i * bits;
-  const int64_t w = (int64_t)(b0 >> 5);
+  const uint64_t b0 = (uint64_t)j * bits;
+  const int64_t w = g * wpg + (int64_t)(b0 >> 5);
   const int sh = (int)(b0 & 31);
   atomicOr(&words[w], (uint32_t)(v << sh));
   if (sh + bits > 32) atomicOr(&words[w + 1], (uint32_t)(v >> (32 - sh)));
 }
 
-__global__ void unpack_bits_kernel(int64_t n, int32_t bits, const uint32_t* __restrict__ words,
-                                   int32_t* __restrict__ idx) {
+__global__ void unpack_bits_kernel(int64_t n, int64_t per, int64_t wpg, int32_t bits,
+                                   const uint32_t* __restrict__ words, int32_t* __restrict__ idx) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint64_t b0 = (uint64_t)i * bits;
-  const int64_t w = (int64_t)(b0 >> 5);
+  const int64_t g = i / per, j = i - g * per;
+  const uint64_t b0 = (uint64_t)j * bits;
+  const int64_t w = g * wpg + (int64_t)(b0 >> 5);
   const int sh = (int)(b0 & 31);
   uint64_t v = words[w] >> sh;
   if (sh + bits > 32) v |= (uint64_t)words[w + 1] << (32 - sh);
@@ -480,24 +484,30 @@ int idf_patch(void* stream, int32_t B, int32_t C, int32_t H, int32_t W, int32_t 
   return idf_last_error();
 }
 
-int64_t idf_pack_bits_words(int64_t n, int32_t bits) { return (n * bits + 31) / 32; }
+int64_t idf_pack_bits_words(int64_t groups, int64_t per, int32_t bits) {
+  return groups * ((per * bits + 31) / 32);
+}
 
-int idf_pack_bits(void* stream, int64_t n, int32_t bits, const int32_t* idx, uint32_t* words) {
-  if (bits < 1 || bits > 31 || n < 0) return IDF_ERR_ARG;
+int idf_pack_bits(void* stream, int64_t groups, int64_t per, int32_t bits, const int32_t* idx,
+                  uint32_t* words) {
+  if (bits < 1 || bits > 31 || groups < 0 || per < 0) return IDF_ERR_ARG;
+  const int64_t n = groups * per;
   if (n == 0) return IDF_OK;
-  if (hipMemsetAsync(words, 0, (size_t)idf_pack_bits_words(n, bits) * 4, (hipStream_t)stream) !=
-      hipSuccess)
+  if (hipMemsetAsync(words, 0, (size_t)idf_pack_bits_words(groups, per, bits) * 4,
+                     (hipStream_t)stream) != hipSuccess)
     return IDF_ERR_HIP;
   hipLaunchKernelGGL(pack_bits_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, n, bits, idx, words);
+                     (hipStream_t)stream, n, per, (per * bits + 31) / 32, bits, idx, words);
   return idf_last_error();
 }
 
-int idf_unpack_bits(void* stream, int64_t n, int32_t bits, const uint32_t* words, int32_t* idx) {
-  if (bits < 1 || bits > 31 || n < 0) return IDF_ERR_ARG;
+int idf_unpack_bits(void* stream, int64_t groups, int64_t per, int32_t bits, const uint32_t* words,
+                    int32_t* idx) {
+  if (bits < 1 || bits > 31 || groups < 0 || per < 0) return IDF_ERR_ARG;
+  const int64_t n = groups * per;
   if (n == 0) return IDF_OK;
   hipLaunchKernelGGL(unpack_bits_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, n, bits, words, idx);
+                     (hipStream_t)stream, n, per, (per * bits + 31) / 32, bits, words, idx);
   return idf_last_error();
 }
 

@@ -81,3 +81,66 @@ def interleave_levels(states, nwords, words, world: int, n_levels: int, per_rank
     pieces = [words[int(off[i]): int(off[i]) + int(nwords[i])] for i in idx]
     w = torch.cat(pieces) if pieces else words[:0]
     return states[idx_t], nwords[idx_t], w
+
+
+def gather_padded(t: torch.Tensor, dst: int = 0, group=None):
+    """Gather a variable-length 1-D tensor from every rank to `dst` (rank order); None elsewhere."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = t.device
+    n_local = torch.tensor([t.numel()], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros_like(n_local) for _ in range(world)]
+    dist.all_gather(sizes, n_local, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    cap = max(max(sizes), 1)
+    padded = torch.zeros(cap, dtype=t.dtype, device=dev)
+    padded[: t.numel()] = t
+    if dist.get_backend(group) == "gloo":
+        bufs = [torch.empty(cap, dtype=t.dtype, device=dev) for _ in range(world)] if rank == dst else None
+        dist.gather(padded, bufs, dst=dst, group=group)
+    else:
+        bufs = [torch.empty(cap, dtype=t.dtype, device=dev) for _ in range(world)]
+        dist.all_gather(bufs, padded, group=group)
+    if rank != dst:
+        return None
+    return torch.cat([b[:s] for b, s in zip(bufs, sizes)])
+
+
+def merge_residual(parts):
+    """Concatenate equal-shaped ResidualBitstreams of consecutive image shards into the
+    single-batch bitstream (flow streams re-ordered level-major / global-image-minor,
+    index code runs concatenated)."""
+    from .codec import Bitstream
+    from .residual import ResidualBitstream
+    fl = [p.flow for p in parts]
+    st = torch.cat([f.states for f in fl])
+    nw = torch.cat([f.nwords.to(torch.int64) for f in fl])
+    w = torch.cat([f.words for f in fl])
+    return _assemble(parts[0], len(parts), st, nw, w, torch.cat([p.idx_words for p in parts]))
+
+
+def _assemble(first, world, st, nw, w, idx):
+    from .codec import Bitstream
+    from .residual import ResidualBitstream
+    fl = first.flow
+    st, nw, w = interleave_levels(st, nw, w, world, len(fl.level_shapes), fl.n_images)
+    meta = {k: v for k, v in fl.meta.items() if k == "n_subpixels"}
+    if "n_subpixels" in meta:
+        meta["n_subpixels"] = meta["n_subpixels"] * world
+    flow = Bitstream(fl.n_images * world, fl.level_shapes, st, nw, w, None, meta)
+    return ResidualBitstream(flow, idx, first.n_images * world, first.image_shape, first.grid,
+                             first.embed_num)
+
+
+def gather_residual(rbs, dst: int = 0, group=None):
+    """Assemble the residual configs' per-shard ResidualBitstreams (idfcodec.residual) on `dst`
+    (RCCL over xGMI with backend nccl): the flow streams via gather_streams, re-ordered to the
+    single-batch order, and the image-aligned index code runs concatenated in rank order.
+    Equal shards required.  Returns the merged bitstream on `dst`, None elsewhere."""
+    world = dist.get_world_size(group)
+    fl = rbs.flow
+    got = gather_streams(fl.states, fl.nwords, fl.words, dst=dst, group=group)
+    idx = gather_padded(rbs.idx_words, dst=dst, group=group)
+    if got is None:
+        return None
+    return _assemble(rbs, world, *got, idx)

@@ -31,7 +31,7 @@ VERSION = 1
 @dataclass
 class ResidualBitstream:
     flow: Bitstream
-    idx_words: torch.Tensor     # int32 view of the packed index words
+    idx_words: torch.Tensor     # int32 view of the packed index words (image-aligned runs)
     n_images: int
     image_shape: tuple          # (C, H, W)
     grid: tuple                 # (h, w) of the VQ indices per image
@@ -126,11 +126,12 @@ class ResidualCodec:
             flow = codec.encode_nchw(res_p, cond=rec_p.contiguous())
         else:
             flow = codec.encode_nchw(res_p)
-        n = idx.numel()
-        words = torch.empty(max(int(lib().idf_pack_bits_words(n, self.bits)), 1),
-                            dtype=torch.int32, device=img_u8.device)
-        check(lib().idf_pack_bits(_lib.stream_ptr(img_u8.device), n, self.bits, ptr(idx),
+        per = idx.shape[1] * idx.shape[2]
+        nwd = int(lib().idf_pack_bits_words(B, per, self.bits))
+        words = torch.empty(max(nwd, 1), dtype=torch.int32, device=img_u8.device)
+        check(lib().idf_pack_bits(_lib.stream_ptr(img_u8.device), B, per, self.bits, ptr(idx),
                                   ptr(words)), "pack idx")
+        words = words[:nwd]
         return ResidualBitstream(flow, words, B, (C, H, W), tuple(idx.shape[1:]),
                                  self.vqvae.embed_num)
 
@@ -142,9 +143,11 @@ class ResidualCodec:
         h, w = rbs.grid
         n = B * h * w
         words = rbs.idx_words.to(dev)
+        if words.numel() == 0:
+            words = torch.zeros(1, dtype=torch.int32, device=dev)
         idx = torch.empty(n, dtype=torch.int32, device=dev)
-        check(lib().idf_unpack_bits(_lib.stream_ptr(dev), n, self.bits, ptr(words), ptr(idx)),
-              "unpack idx")
+        check(lib().idf_unpack_bits(_lib.stream_ptr(dev), B, h * w, self.bits, ptr(words),
+                                    ptr(idx)), "unpack idx")
         rec = self.vqvae.reconstruct(idx.view(B, h, w))
         codec = self._codec()
         if self.conditional:

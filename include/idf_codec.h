@@ -320,12 +320,15 @@ int idf_vq_gather(void *stream, int64_t P, int32_t D, const int32_t *d_idx, cons
  * 2 x - z, 3 x + z (trainer.py:606-608 residual split and its inverse). */
 int idf_vq_pointwise(void *stream, int64_t P, int32_t C, int32_t op, const float *d_x, int64_t ld_x,
                      const float *d_z, int64_t ld_z, float *d_y, int64_t ld_y);
-/* Fixed-width code of the VQ indices (absent in the reference): index i
- * occupies bits [i*bits, (i+1)*bits) of a little-endian uint32 stream of
- * idf_pack_bits_words(n, bits) words; 1 <= bits <= 31. */
-int64_t idf_pack_bits_words(int64_t n, int32_t bits);
-int idf_pack_bits(void *stream, int64_t n, int32_t bits, const int32_t *d_idx, uint32_t *d_words);
-int idf_unpack_bits(void *stream, int64_t n, int32_t bits, const uint32_t *d_words, int32_t *d_idx);
+/* Fixed-width code of the VQ indices (absent in the reference): `groups`
+ * runs (one per image) of `per` indices; run g starts at word g*ceil(per*bits/32) and its
+ * index j occupies bits [j*bits, (j+1)*bits) of that little-endian uint32 run, so images'
+ * (and shards') codes concatenate.  1 <= bits <= 31. */
+int64_t idf_pack_bits_words(int64_t groups, int64_t per, int32_t bits);
+int idf_pack_bits(void *stream, int64_t groups, int64_t per, int32_t bits, const int32_t *d_idx,
+                  uint32_t *d_words);
+int idf_unpack_bits(void *stream, int64_t groups, int64_t per, int32_t bits,
+                    const uint32_t *d_words, int32_t *d_idx);
 /* Patching.forward / backward (extenddim.py:52-67) on NCHW: [B,C,H,W] <-> [B*(H/h)*(W/w),C,h,w]. */
 int idf_patch(void *stream, int32_t B, int32_t C, int32_t H, int32_t W, int32_t h, int32_t w,
               int32_t inverse, const float *d_src, float *d_dst);

@@ -82,3 +82,40 @@ def test_shard_range_covers():
             rs = [shard_range(n, r, world) for r in range(world)]
             assert rs[0][0] == 0 and rs[-1][1] == n
             assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
+
+
+def _res_worker(rank, world, port, out):
+    import sys
+    sys.path.insert(0, PKG)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from idfcodec.codec import Bitstream
+    from idfcodec.dist import gather_residual
+    from idfcodec.residual import ResidualBitstream
+    st, nw, w = _fake_shard(rank, 2, 3)
+    flow = Bitstream(3, [(6, 4, 4), (12, 2, 2)], st, nw, w, meta={"n_subpixels": 3 * 192})
+    idx = torch.arange(5, dtype=torch.int32) + 100 * rank  # 5 words: 3 images x 1..2 words
+    rbs = ResidualBitstream(flow, idx, 3, (3, 8, 8), (2, 2), 8192)
+    res = gather_residual(rbs)
+    if rank == 0:
+        torch.save({"st": res.flow.states, "idx": res.idx_words, "n": res.n_images,
+                    "ns": res.flow.meta["n_subpixels"]}, out)
+    else:
+        assert res is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_residual_two_ranks(tmp_path):
+    """configs 4/5 (8 x MI355X, batch-sharded): the residual bitstreams of two ranks merge on
+    rank 0 -- flow streams in single-batch order, index code runs in rank order."""
+    out = str(tmp_path / "r.pt")
+    mp.spawn(_res_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    r = torch.load(out, weights_only=True)
+    assert r["n"] == 6 and r["ns"] == 6 * 192
+    assert torch.equal(r["idx"], torch.cat([torch.arange(5) + 100 * k for k in range(2)]).int())
+    parts = [_fake_shard(k, 2, 3) for k in range(2)]
+    for l in range(2):
+        for rnk in range(2):
+            for b in range(3):
+                assert r["st"][l * 6 + rnk * 3 + b] == parts[rnk][0][l * 3 + b]

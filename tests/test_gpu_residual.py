@@ -63,3 +63,22 @@ def test_config3_round_trip():
     out, info = codec.decode(ResidualBitstream.from_bytes(rbs.to_bytes(), device="cuda"))
     assert info["ok"] and torch.equal(out, x)
     assert rbs.index_bits == 14
+
+
+def test_residual_shards_merge_to_one_bitstream():
+    """Two shards coded separately (the per-rank work of configs 4/5) merge into the
+    bitstream of the whole batch (idfcodec.dist.merge_residual, the core of gather_residual)."""
+    from idfcodec import synthetic
+    from idfcodec.dist import merge_residual
+    from idfcodec.residual import ResidualCodec
+    fl = _flows("IDFlows", 16, 16, 2)
+    vq = _vq_small([8, 16], K=100)       # 7-bit indices: runs not word-aligned per index
+    codec = ResidualCodec(fl, vq, (32, 32))
+    x = synthetic.images(4, H=32, W=32, seed=33).cuda()
+    parts = [codec.encode(x[:2]), codec.encode(x[2:])]
+    merged = merge_residual(parts)
+    out, info = codec.decode(merged)
+    assert info["ok"] and torch.equal(out, x)
+    whole = codec.encode(x)
+    assert torch.equal(merged.idx_words.cpu(), whole.idx_words.cpu())
+    assert torch.equal(merged.flow.states.cpu(), whole.flow.states.cpu())
