@@ -577,7 +577,13 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
     if (blk->fold) {  // one launch per layer: 3x3 over the layer input, 1x1 folded in
       timer_mark(timer, s, IDF_TAG_CONV3X3, 2.0 * P * 9.0 * cr * gr, true);
       const bool wino = blk->wino && blk->wino_u[i] && idf_conv3x3_wino_supported(H, W);
-      int rc = wino
+      const bool bf = blk->bf16 && blk->wb16[i];
+      int rc = bf
+                   ? idf_conv3x3_bf16(stream, B, H, W, c, feat, ld_feat, blk->wb16[i],
+                                      blk->g_alloc, blk->b3[i], blk->vtap[i], blk->ldv,
+                                      blk->bfull[i], blk->g_pad, feat + c, ld_feat, blk->act,
+                                      blk->slope, tmp, P * ld_tmp)
+               : wino
                    ? idf_conv3x3_wino(stream, B, H, W, c, feat, ld_feat, blk->wino_u[i],
                                       blk->wino_nft, blk->b3[i], blk->vtap[i], blk->ldv,
                                       blk->bfull[i], blk->g_pad, feat + c, ld_feat, blk->act,

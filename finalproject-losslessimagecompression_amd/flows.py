@@ -86,7 +86,8 @@ class IDFlows(nn.Module):
         if dev.type != "cuda":
             raise RuntimeError("idfcodec: move the model to the HIP device (.cuda()) first; "
                                "there is no CPU path")
-        key = tuple((p.data_ptr(), p._version) for p in self.parameters())
+        key = tuple((p.data_ptr(), p._version) for p in self.parameters()) + (
+            getattr(self, "idf_precision", "f32"),)
         if self._engine is None or self._engine_key != key:
             self._engine = FlowEngine(self, dev)
             self._engine_key = key

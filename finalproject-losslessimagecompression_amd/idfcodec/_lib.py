@@ -52,6 +52,7 @@ class IdfDenseBlock(ctypes.Structure):
         ("c_real", i32 * (MAX_DEPTH + 1)), ("g_real", i32 * MAX_DEPTH),
         ("fold", i32), ("ldv", i32), ("vtap", P * MAX_DEPTH), ("bfull", P * MAX_DEPTH),
         ("halo", i32), ("wino", i32), ("wino_nft", i32), ("wino_u", P * MAX_DEPTH),
+        ("bf16", i32), ("wb16", P * MAX_DEPTH),
     ]
 
 
@@ -95,6 +96,9 @@ SIGNATURES = {
     "idf_conv3x3_wino_supported": (ctypes.c_int, [i32, i32]),
     "idf_conv3x3_wino_workspace": (i64, [i32, i32, i32, i32, i32]),
     "idf_conv3x3_wino": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, P, P, i32, P, i32, P,
+                                        i64, i32, f32, P, i64]),
+    "idf_conv3x3_bf16_workspace": (i64, [i32, i32, i32, i32, i32]),
+    "idf_conv3x3_bf16": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, P, P, i32, P, i32, P,
                                         i64, i32, f32, P, i64]),
     "idf_dequant_u8": (ctypes.c_int, [P, i32, i32, i32, i32, P, P, i64]),
     "idf_quant_u8": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, P]),

@@ -63,6 +63,10 @@ VQVAE = {
 }
 
 
+# BASELINE configs[2] names "MFMA bf16 coupling convs with fp32 CDF" for this config
+PRECISION = {"resflow-cond-imagenet64": "bf16"}
+
+
 def get(name: str) -> dict:
     return copy.deepcopy(CONFIGS[name])
 

@@ -55,6 +55,7 @@ class DeviceBlock:
         self.vtap = [dev(a) for a in packed.vtap]
         self.bfull = [dev(a) for a in packed.bfull]
         self.wino_u = [dev(a) for a in packed.wino_u]
+        self.wb16 = [dev(a.view(np.int16)) for a in packed.wb16]
         d = IdfDenseBlock()
         g = self.geom
         d.depth = g.depth
@@ -89,6 +90,9 @@ class DeviceBlock:
         d.wino_nft = packed.g_alloc // 16
         for i, u in enumerate(self.wino_u):
             d.wino_u[i] = u.data_ptr()
+        d.bf16 = 1 if (packed.fold and self.wb16) else 0
+        for i, u in enumerate(self.wb16):
+            d.wb16[i] = u.data_ptr()
         d.ldv = packed.g_alloc
         for i in range(len(self.vtap)):
             d.vtap[i] = self.vtap[i].data_ptr()
@@ -150,8 +154,15 @@ class FlowEngine:
 
     def __init__(self, model, device=None, fold: bool | None = None):
         self.device = torch.device(device or "cuda")
+        # "bf16": the DenseLayer convs run on bf16 MFMA (configs naming bf16 coupling convs,
+        # e.g. resflow-cond-imagenet64); "f32" (default): fp32, within 1e-5 of the reference
+        self.precision = getattr(model, "idf_precision", "f32")
+        if self.precision not in ("f32", "bf16"):
+            raise ValueError(f"idf_precision must be 'f32' or 'bf16', not {self.precision!r}")
         self.fold = FOLD if fold is None else bool(fold)
-        self.wino = self.fold and WINO and any(
+        if self.precision == "bf16":
+            self.fold = True
+        self.wino = self.fold and WINO and self.precision == "f32" and any(
             lib().idf_conv3x3_wino_supported(model.H // s, model.W // s)
             for s in [model.blocks[0]["extend"].scale ** (l + 1) for l in range(model.nsplit)])
         sd = {k: v for k, v in model.state_dict().items()}
@@ -191,10 +202,11 @@ class FlowEngine:
         for l in range(self.nsplit):
             self.couple.append([DeviceBlock(pack_dense_block(
                 sd, f"blocks.{l}.flows.{2 * k + 1}.dense.", c_depth, c_act, fold=self.fold,
-                wino=self.wino),
+                wino=self.wino, bf16=self.precision == "bf16"),
                 self.device) for k in range(self.nflows)])
             self.prior.append(DeviceBlock(pack_dense_block(sd, f"blocks.{l}.prior.NN.", p_depth,
-                                                           p_act, fold=self.fold, wino=self.wino),
+                                                           p_act, fold=self.fold, wino=self.wino,
+                                                           bf16=self.precision == "bf16"),
                                           self.device))
             ids_l, inv_l = [], []
             for k in range(self.nflows + 1):

@@ -111,6 +111,7 @@ class PackedBlock:
     nh_alloc: int
     ldwh: int
     wino_u: list = field(default_factory=list)  # fold+wino: wino_weights() per layer
+    wb16: list = field(default_factory=list)    # fold+bf16: bf16_weights() per layer (uint16)
 
 
 def fold_layer(w1, b1, w3):
@@ -154,6 +155,21 @@ def wino_weights(w: np.ndarray, nslab: int) -> np.ndarray:
     return np.ascontiguousarray(U.reshape(16, nslab, nft, 64, 4).astype(np.float32))
 
 
+def bf16_weights(w: np.ndarray, C: int) -> np.ndarray:
+    """w: [n_alloc][9][ldw] fp32 folded 3x3 weights (padded coordinates), C = the layer's
+    padded input channels.  Returns uint16 bf16 bits (round to nearest even) in the fragment
+    order of conv3_bf16.hip: [ceil(C/32) slabs][9 taps][4 k-blocks][n_alloc][8 channels]."""
+    import torch
+    n_alloc = w.shape[0]
+    nslab = (C + 31) // 32
+    g = np.zeros((n_alloc, 9, nslab * 32), np.float32)
+    cw = min(w.shape[2], C)
+    g[:, :, :cw] = w[:, :, :cw]
+    b = torch.from_numpy(g).to(torch.bfloat16).view(torch.int16).numpy().view(np.uint16)
+    b = b.reshape(n_alloc, 9, nslab, 4, 8).transpose(2, 1, 3, 0, 4)  # slab, tap, kb, n, e
+    return np.ascontiguousarray(b)
+
+
 def interior_bias(b3: np.ndarray, v: np.ndarray) -> np.ndarray:
     """b3 + v[0] + ... + v[8], sequential fp32 adds: the order the device's border
     loop uses, so interior and border pixels see the same arithmetic."""
@@ -164,7 +180,8 @@ def interior_bias(b3: np.ndarray, v: np.ndarray) -> np.ndarray:
 
 
 def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
-                     slope: float = 0.01, fold: bool = False, wino: bool = False) -> PackedBlock:
+                     slope: float = 0.01, fold: bool = False, wino: bool = False,
+                     bf16: bool = False) -> PackedBlock:
     """Pack the reference DenseBlock parameters found under `prefix` in `sd`
     (keys `{prefix}layers.{i}.layers.{0,1}.{weight,bias}`, head `{prefix}layers.{depth}.*`).
     fold=True folds each layer's 1x1 conv into its 3x3 conv (fold_layer)."""
@@ -182,7 +199,7 @@ def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
     geom = BlockGeometry(a=a, depth=depth, growth=gs, n_head=n_head)
     g_alloc = round_up(geom.g_pad, tile_n(geom.g_pad))
     w1s, b1s, w3s, b3s, n1s, ld1s, ld3s = [], [], [], [], [], [], []
-    vts, bfs, wus = [], [], []
+    vts, bfs, wus, wbs = [], [], [], []
     c = a
     for i in range(depth):
         k = geom.k_in[i]
@@ -211,6 +228,8 @@ def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
                 w64 = np.zeros((g_alloc, 9, ldw3), np.float64)
                 w64[:g][:, :, pos] = wf64
                 wus.append(wino_weights(w64, ldw3 // 16))
+            if bf16:
+                wbs.append(bf16_weights(w3p, k))
             vp = np.zeros((9, g_alloc), np.float32)
             vp[:, :g] = v
             vts.append(vp)
@@ -229,7 +248,7 @@ def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
     bhp = np.zeros(nh_alloc, np.float32)
     bhp[:n_head] = arr(f"layers.{depth}.bias")
     return PackedBlock(geom, act, slope, fold, vts, bfs, w1s, b1s, w3s, b3s, whp, bhp, g_alloc,
-                       n1s, ld1s, ld3s, nh_alloc, ldwh, wus)
+                       n1s, ld1s, ld3s, nh_alloc, ldwh, wus, wbs)
 
 
 def unpack_features(feat: np.ndarray, geom: BlockGeometry, n: int) -> np.ndarray:

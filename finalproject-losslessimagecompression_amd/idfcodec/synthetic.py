@@ -51,11 +51,14 @@ def build_vqvae(cfg: dict, seed: int = 0):
     return EnDecoder.get(cfg.pop("name"))(**cfg).eval()
 
 
-def build_residual(name: str, device="cuda"):
-    """(ResidualCodec, flows model, vqvae, input_size) of a residual north-star config."""
+def build_residual(name: str, device="cuda", precision: str | None = None):
+    """(ResidualCodec, flows model, vqvae, input_size) of a residual north-star config.
+    precision: the flow's DenseLayer arithmetic ("f32" | "bf16"); default: the config's
+    (bf16 for resflow-cond-imagenet64, BASELINE configs[2]; f32 otherwise)."""
     from idfcodec import configs
     from idfcodec.residual import ResidualCodec
     vcfg, size = configs.get_vqvae(name)
     flows_model = build_model(configs.get(name)).to(device)
+    flows_model.idf_precision = precision or configs.PRECISION.get(name, "f32")
     vq = build_vqvae(vcfg).to(device)
     return ResidualCodec(flows_model, vq, size), flows_model, vq, size

@@ -165,6 +165,10 @@ typedef struct IdfDenseBlock {
   int32_t wino;
   int32_t wino_nft;
   const float *wino_u[IDF_MAX_DEPTH];
+  /* bf16 = 1 (with fold = 1): the folded 3x3 runs on bf16 MFMA (idf_conv3x3_bf16) with the
+   * fragment-ordered bf16 weights wb16[i] -- for configs that name bf16 coupling convs */
+  int32_t bf16;
+  const uint16_t *wb16[IDF_MAX_DEPTH];
 } IdfDenseBlock;
 
 /* Head epilogue target */
@@ -252,6 +256,18 @@ int idf_conv3x3_wino_supported(int32_t H, int32_t W);
 int64_t idf_conv3x3_wino_workspace(int32_t B, int32_t H, int32_t W, int32_t C, int32_t N);
 int idf_conv3x3_wino(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, const float *d_x,
                      int64_t ld_x, const float *d_u, int32_t nft, const float *d_b3,
+                     const float *d_vtap, int32_t ldv, const float *d_bfull, int32_t N,
+                     float *d_out, int64_t ld_out, int32_t act, float slope, float *d_workspace,
+                     int64_t workspace_floats);
+
+/* The same folded 3x3 conv on bf16 MFMA (v_mfma_f32_16x16x32_bf16, fp32 accumulation): X is
+ * read as fp32 and rounded to bf16 (nearest even) on its way into LDS; d_wb holds the
+ * weights rounded to bf16 in fragment order [ceil(C/32)][9][4][n_alloc][8]
+ * (idfcodec/packing.py bf16_weights), n_alloc = 16*ceil(N/16) <= 48.  For the configs that
+ * name bf16 coupling convs (resflow-cond-imagenet64); deterministic and batch-invariant. */
+int64_t idf_conv3x3_bf16_workspace(int32_t B, int32_t H, int32_t W, int32_t C, int32_t N);
+int idf_conv3x3_bf16(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, const float *d_x,
+                     int64_t ld_x, const uint16_t *d_wb, int32_t n_alloc, const float *d_b3,
                      const float *d_vtap, int32_t ldv, const float *d_bfull, int32_t N,
                      float *d_out, int64_t ld_out, int32_t act, float slope, float *d_workspace,
                      int64_t workspace_floats);

@@ -1,0 +1,87 @@
+"""GPU parity of the bf16-MFMA DenseLayer conv (conv3_bf16.hip) against fp64 conv2d of the
+bf16-rounded operands (products of bf16 values are exact in fp32; only the fp32
+accumulation differs: 1e-5), its batch invariance (what makes the bf16 codec lossless), and
+lossless round trips of the bf16 flow (BASELINE configs[2] names bf16 coupling convs)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(X, Wt, b3, vt, bfull, B, H, W, C, N, act="ReLU"):
+    from idfcodec import _lib
+    from idfcodec._lib import check, lib, ptr
+    from idfcodec.packing import bf16_weights, round_up
+    ld = X.shape[1]
+    n_alloc = round_up(N, 16)
+    wb = torch.from_numpy(bf16_weights(Wt.numpy().astype(np.float32), C).view(np.int16)).cuda()
+    dev = torch.device("cuda")
+    Xd, b3d = X.to(dev), b3.to(dev)
+    vtd = vt.to(dev) if vt is not None else None
+    bfd = bfull.to(dev) if bfull is not None else None
+    out = torch.zeros(B * H * W, ld, device=dev)
+    wsn = lib().idf_conv3x3_bf16_workspace(B, H, W, C, N)
+    ws = torch.empty(max(wsn, 1), device=dev)
+    check(lib().idf_conv3x3_bf16(_lib.stream_ptr(), B, H, W, C, ptr(Xd), ld, ptr(wb), n_alloc,
+                                 ptr(b3d), ptr(vtd), n_alloc, ptr(bfd), N, ptr(out), ld,
+                                 _lib.ACT[act], 0.01, ptr(ws), wsn), "bf16 conv")
+    torch.cuda.synchronize()
+    return out.cpu()
+
+
+@pytest.mark.parametrize("B,H,W,C,N,fold", [
+    (3, 32, 32, 52, 43, True), (5, 16, 16, 100, 43, True), (9, 8, 8, 168, 43, True),
+    (2, 6, 10, 24, 20, False), (1, 16, 16, 520, 43, True)])
+def test_conv3x3_bf16_vs_fp64(B, H, W, C, N, fold):
+    g = torch.Generator().manual_seed(B * 5 + H + C)
+    ld = ((C + N + 15) // 16) * 16 + 4
+    X = torch.randn(B * H * W, ld, generator=g)
+    n_alloc = ((N + 15) // 16) * 16
+    ldw = ((C + 15) // 16) * 16
+    Wt = torch.randn(n_alloc, 9, ldw, generator=g) / np.sqrt(9 * C)
+    Wt[:, :, C:] = 0
+    b3 = torch.randn(n_alloc, generator=g) * 0.1
+    vt = torch.randn(9, n_alloc, generator=g) * 0.1 if fold else None
+    bfull = None
+    if fold:
+        s = b3.clone()
+        for t in range(9):
+            s = s + vt[t]
+        bfull = s
+    out = _run(X, Wt, b3, vt, bfull, B, H, W, C, N)
+    xr = X[:, :C].to(torch.bfloat16).double().view(B, H, W, C).permute(0, 3, 1, 2)
+    wr = Wt[:N, :, :C].to(torch.bfloat16).double().permute(0, 2, 1).reshape(N, C, 3, 3)
+    ref = F.conv2d(xr, wr, padding=1) + b3[:N].double().view(1, -1, 1, 1)
+    if fold:
+        mask = F.conv2d(torch.ones(1, 1, H, W, dtype=torch.float64),
+                        torch.eye(9, dtype=torch.float64).view(9, 1, 3, 3), padding=1)
+        ref = ref + torch.einsum("tn,bthw->bnhw", vt[:, :N].double(), mask)
+    ref = F.relu(ref)
+    got = out[:, :N].double().view(B, H, W, N).permute(0, 3, 1, 2)
+    err = ((got - ref).abs() / ref.abs().clamp(min=1.0)).max().item()
+    assert err <= 1e-5, err
+    assert torch.all(out[:, N:] == 0)
+
+
+def test_conv3x3_bf16_batch_invariant():
+    g = torch.Generator().manual_seed(7)
+    B, H, W, C, N = 6, 8, 8, 100, 43
+    ld = 160
+    X = torch.randn(B * H * W, ld, generator=g)
+    Wt = torch.randn(48, 9, 112, generator=g) / 30
+    b3 = torch.randn(48, generator=g) * 0.1
+    full = _run(X, Wt, b3, None, None, B, H, W, C, N)
+    one = _run(X[2 * 64: 3 * 64].contiguous(), Wt, b3, None, None, 1, H, W, C, N)
+    assert torch.equal(full[2 * 64: 3 * 64], one)
+
+
+def test_bf16_flow_round_trip_config3():
+    """resflow-cond-imagenet64 with bf16 coupling convs (its BASELINE precision), B=2."""
+    from idfcodec import synthetic
+    codec, fl, vq, size = synthetic.build_residual("resflow-cond-imagenet64")
+    assert fl.engine().precision == "bf16"
+    x = synthetic.images(2, H=size[0], W=size[1], seed=8).cuda()
+    out, info = codec.decode(codec.encode(x))
+    assert info["ok"] and torch.equal(out, x)

@@ -257,3 +257,26 @@ def test_restated_expf_equals_libm_on_all_floats(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
     assert "mismatches=0" in r.stdout
+
+
+def test_bf16_weight_packing_layout():
+    """bf16_weights: uint16 bf16 bits of the fp32 folded weights in the fragment order
+    [slab][tap][k-block][n][8] that conv3_bf16.hip reads."""
+    import numpy as np
+    import torch
+    from idfcodec.packing import bf16_weights
+    rng = np.random.default_rng(4)
+    n_alloc, C, ldw = 48, 52, 64
+    w = rng.normal(0, 1, (n_alloc, 9, ldw)).astype(np.float32)
+    w[:, :, C:] = 0
+    b = bf16_weights(w, C)
+    nslab = (C + 31) // 32
+    assert b.shape == (nslab, 9, 4, n_alloc, 8) and b.dtype == np.uint16
+    ref = torch.from_numpy(w).to(torch.bfloat16).float().numpy()
+    back = torch.from_numpy(b.astype(np.int16)).view(torch.bfloat16).float().numpy()
+    for s in range(nslab):
+        for kb in range(4):
+            for e in range(8):
+                c = 32 * s + 8 * kb + e
+                want = ref[:, :, c] if c < C else np.zeros((n_alloc, 9), np.float32)
+                assert np.array_equal(back[s, :, kb, :, e].T, want)

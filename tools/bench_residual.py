@@ -4,8 +4,9 @@ Default: resflow-cond-imagenet64 (configs[2]), batch 1024 synthetic 64x64x3 uint
 weights (the configs' checkpoints are absent).  One step = ResidualCodec.encode then
 decode of the batch, inputs resident in HBM.  Prints one JSON line: Mpx/s (encode+decode),
 the encode / decode split, the VQ-VAE share of each, bits per pixel (flow streams + index
-code) and the exactness of the round trip.  The flow here is fp32 (the config names bf16
-MFMA coupling convs -- see DESIGN.md).
+code) and the exactness of the round trip.  The flow's DenseLayer convs run in the config's
+precision (bf16 MFMA for resflow-cond-imagenet64, as BASELINE configs[2] names; --precision
+overrides).
 
   python tools/bench_residual.py [--config NAME] [--batch B] [--steps K] [--warmup W]
 """
@@ -29,9 +30,10 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--precision", default=None, choices=[None, "f32", "bf16"])
     a = ap.parse_args()
     from idfcodec import synthetic
-    codec, fl, vq, (H, W) = synthetic.build_residual(a.config)
+    codec, fl, vq, (H, W) = synthetic.build_residual(a.config, precision=a.precision)
     img = synthetic.images(a.batch, H=H, W=W, seed=2).cuda()
 
     def vq_time(B):
@@ -70,7 +72,10 @@ def main():
         "vq_indices_ms": round(t_idx * 1e3, 2), "vq_reconstruct_ms": round(t_rec * 1e3, 2),
         "bpp": round(3 * rbs.bpd(), 4), "index_bits_share": round(
             1 - rbs.flow.bits() / rbs.bits(), 4),
-        "round_trip_exact": exact, "dtype": "f32", "data": "synthetic uint8, seeded weights"}),
+        "round_trip_exact": exact,
+        "dtype": ("bf16 flow convs (f32 accumulate), f32 heads/VQ-VAE/CDF"
+                  if fl.engine().precision == "bf16" else "f32"),
+        "data": "synthetic uint8, seeded weights"}),
         flush=True)
 
 

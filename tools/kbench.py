@@ -1,7 +1,7 @@
 """Kernel microbenchmark of the folded 3x3 conv at the imagenet64 shapes (B=256): the LDS
 halo-tiled kernel (idf_conv3x3_halo) and the implicit-GEMM kernel (idf_conv3x3_fold_f32),
 per level and layer width.  Prints achieved TFLOP/s (unpadded FLOPs).
-Env filters: KB_ONLY=wino,halo,gemm  KB_LEVELS=0,1,2  KB_LAYERS=0,3,6,9,11  KB_REPS=10."""
+Env filters: KB_ONLY=wino,halo,gemm,bf16  KB_LEVELS=0,1,2  KB_LAYERS=0,3,6,9,11  KB_REPS=10."""
 import os
 import sys
 
@@ -33,7 +33,7 @@ def main():
     dev = torch.device("cuda")
     s = _lib.stream_ptr()
     g_pad, g_alloc, g_real = 44, 48, 43
-    only = os.environ.get("KB_ONLY", "wino,halo,gemm").split(",")
+    only = os.environ.get("KB_ONLY", "wino,halo,gemm,bf16").split(",")
     layers = [int(v) for v in os.environ.get("KB_LAYERS", "0,3,6,9,11").split(",")]
     levels = [int(v) for v in os.environ.get("KB_LEVELS", "0,1,2").split(",")]
     reps = int(os.environ.get("KB_REPS", "10"))
@@ -72,12 +72,23 @@ def main():
                                              ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
                                              ptr(feat) + c_pad * 4, ld, 0, 0.0, ptr(wws), wwn), "wino")
 
+            from idfcodec.packing import bf16_weights
+            WB = torch.from_numpy(bf16_weights(np.random.default_rng(1).normal(
+                0, 0.01, (g_alloc, 9, ldw)).astype(np.float32), c_pad).view(np.int16)).to(dev)
+            bwn = lib().idf_conv3x3_bf16_workspace(B, hw, hw, c_pad, g_pad)
+            bws = torch.empty(max(bwn, 1), device=dev)
+
+            def bf16():
+                check(lib().idf_conv3x3_bf16(s, B, hw, hw, c_pad, ptr(feat), ld, ptr(WB), g_alloc,
+                                             ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
+                                             ptr(feat) + c_pad * 4, ld, 0, 0.0, ptr(bws), bwn), "bf16")
+
             def gemm():
                 check(lib().idf_conv3x3_fold_f32(s, B, hw, hw, c_pad, ptr(feat), ld, ptr(w), ldw,
                                                  g_alloc, ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
                                                  ptr(feat) + c_pad * 4, ld, 0, 0.0), "gemm")
             line = f"L{lvl} hw={hw:2d} c={c_pad:4d} P={P:7d}"
-            for name, fn in (("wino", wino), ("halo", halo), ("gemm", gemm)):
+            for name, fn in (("wino", wino), ("halo", halo), ("gemm", gemm), ("bf16", bf16)):
                 if name not in only:
                     continue
                 ms = time_it(fn, reps)
