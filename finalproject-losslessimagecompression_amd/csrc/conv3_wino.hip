@@ -449,16 +449,25 @@ struct WinoPlan {
   int ok, IMGS, TH, TW, ksplit;
 };
 
-// Output tile and split for an image geometry (never the batch size).
+// Output tile and split for an image geometry (never the batch size).  Odd H or W are
+// tiled as the next even size: the extra row/column of 2x2 tiles reads zero padding
+// (out-of-image halo) and its outputs are never stored, so every stored pixel sees the
+// same 3x3 neighbourhood as in the direct conv.
 static WinoPlan wino_plan(int H, int W, int nslab) {
   WinoPlan pl = {0, 1, 0, 0, 1};
-  if ((H & 1) || (W & 1) || H < 2 || W < 2) return pl;
-  pl.TW = W < 32 ? W : 32;
+  if (H < 1 || W < 1) return pl;
+  const int He = (H + 1) & ~1, We = (W + 1) & ~1;
+  pl.TW = We < 32 ? We : 32;
   pl.TH = 256 / pl.TW;  // 64 wino tiles = 256 output pixels
-  if (pl.TH > H) pl.TH = H;
+  if (pl.TH > He) pl.TH = He;
   if (pl.TH & 1) pl.TH -= 1;
   if (pl.TH < 2) return pl;
-  if (pl.TH == H) {
+  if (pl.TH < He) {
+    // balance the row tiles: same tile count, least overhang below the image
+    const int nty = (He + pl.TH - 1) / pl.TH;
+    pl.TH = ((He + nty - 1) / nty + 1) & ~1;
+  }
+  if (pl.TH == He) {
     pl.IMGS = 256 / (pl.TH * pl.TW);
     if (pl.IMGS < 1) pl.IMGS = 1;
   }

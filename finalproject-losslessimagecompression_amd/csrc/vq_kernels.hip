@@ -369,6 +369,20 @@ __global__ void patch_kernel(int32_t B, int32_t C, int32_t H, int32_t W, int32_t
   else dst[j] = src[i];
 }
 
+// ReplicationPad2d(padding=(0, right, 0, bottom)) of uint8 NCHW images (trainer.py:62,69-70:
+// the dataloader pads the right/bottom edges by replication before Round) when Ho >= Hi and
+// Wo >= Wi; the same map with Ho <= Hi, Wo <= Wi is the crop that undoes it.
+__global__ void pad_edge_u8_kernel(int64_t total, int32_t Hi, int32_t Wi, int32_t Ho, int32_t Wo,
+                                   const uint8_t* __restrict__ src, uint8_t* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int x = (int)(i % Wo);
+  const int64_t t = i / Wo;
+  const int y = (int)(t % Ho);
+  const int64_t bc = t / Ho;
+  dst[i] = src[(bc * Hi + min(y, Hi - 1)) * Wi + min(x, Wi - 1)];
+}
+
 // Fixed-width index code (the VQ indices of the residual configs):
 // indices come in groups (one image each) of `per` indices; group g starts at word
 // g * wpg (wpg = ceil(per * bits / 32)), and its index j occupies bits
@@ -481,6 +495,17 @@ int idf_patch(void* stream, int32_t B, int32_t C, int32_t H, int32_t W, int32_t 
   if (n <= 0) return IDF_OK;
   hipLaunchKernelGGL(patch_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, B, C, H, W, h, w, inverse, src, dst);
+  return idf_last_error();
+}
+
+int idf_pad_edge_u8(void* stream, int32_t B, int32_t C, int32_t Hi, int32_t Wi, int32_t Ho,
+                    int32_t Wo, const uint8_t* src, uint8_t* dst) {
+  if (B < 0 || C < 0 || Hi <= 0 || Wi <= 0 || Ho <= 0 || Wo <= 0) return IDF_ERR_ARG;
+  if ((Ho - Hi) * (long)(Wo - Wi) < 0) return IDF_ERR_ARG;  // pad both or crop both
+  const int64_t n = (int64_t)B * C * Ho * Wo;
+  if (n == 0) return IDF_OK;
+  hipLaunchKernelGGL(pad_edge_u8_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, n, Hi, Wi, Ho, Wo, src, dst);
   return idf_last_error();
 }
 

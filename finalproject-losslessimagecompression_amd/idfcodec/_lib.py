@@ -118,6 +118,7 @@ SIGNATURES = {
     "idf_vq_gather": (ctypes.c_int, [P, i64, i32, P, P, i32, P, i64]),
     "idf_vq_pointwise": (ctypes.c_int, [P, i64, i32, i32, P, i64, P, i64, P, i64]),
     "idf_patch": (ctypes.c_int, [P, i32, i32, i32, i32, i32, i32, i32, P, P]),
+    "idf_pad_edge_u8": (ctypes.c_int, [P, i32, i32, i32, i32, i32, i32, P, P]),
     "idf_pack_bits_words": (i64, [i64, i64, i32]),
     "idf_pack_bits": (ctypes.c_int, [P, i64, i64, i32, P, P]),
     "idf_unpack_bits": (ctypes.c_int, [P, i64, i64, i32, P, P]),

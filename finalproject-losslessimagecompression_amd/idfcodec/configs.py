@@ -65,6 +65,9 @@ VQVAE = {
 
 # BASELINE configs[2] names "MFMA bf16 coupling convs with fp32 CDF" for this config
 PRECISION = {"resflow-cond-imagenet64": "bf16"}
+# dataloader ReplicationPad2d (bottom, right) before coding (trainer.py:62; the 215x178
+# CelebA crops of configs/resflow-patches-vqvae.yaml:84-93 become 216x184)
+PAD = {"resflow-patches-vqvae": (1, 6)}
 
 
 def get(name: str) -> dict:

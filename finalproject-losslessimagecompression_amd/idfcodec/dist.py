@@ -129,7 +129,7 @@ def _assemble(first, world, st, nw, w, idx):
         meta["n_subpixels"] = meta["n_subpixels"] * world
     flow = Bitstream(fl.n_images * world, fl.level_shapes, st, nw, w, None, meta)
     return ResidualBitstream(flow, idx, first.n_images * world, first.image_shape, first.grid,
-                             first.embed_num)
+                             first.embed_num, first.source_hw)
 
 
 def gather_residual(rbs, dst: int = 0, group=None):

@@ -25,7 +25,7 @@ from ._lib import check, lib, ptr
 from .codec import Bitstream, ImageCodec
 
 MAGIC = b"IDFR"
-VERSION = 1
+VERSION = 2         # 2 adds the source (pre-pad) image size; version-1 streams still read
 
 
 @dataclass
@@ -36,6 +36,12 @@ class ResidualBitstream:
     image_shape: tuple          # (C, H, W)
     grid: tuple                 # (h, w) of the VQ indices per image
     embed_num: int
+    source_hw: tuple | None = None   # (H, W) before the dataloader's replication pad
+
+    @property
+    def source_shape(self) -> tuple:
+        C, H, W = self.image_shape
+        return (C,) + tuple(self.source_hw or (H, W))
 
     @property
     def index_bits(self) -> int:
@@ -51,8 +57,9 @@ class ResidualBitstream:
 
     def to_bytes(self) -> bytes:
         C, H, W = self.image_shape
-        hdr = struct.pack("<4sHHIIIIIII", MAGIC, VERSION, 0, self.n_images, C, H, W,
-                          self.grid[0], self.grid[1], self.embed_num)
+        sh, sw = self.source_hw or (H, W)
+        hdr = struct.pack("<4sHHIIIIIIIII", MAGIC, VERSION, 0, self.n_images, C, H, W,
+                          self.grid[0], self.grid[1], self.embed_num, sh, sw)
         iw = self.idx_words.detach().cpu().numpy().astype("<i4").tobytes()
         fb = self.flow.to_bytes()
         return hdr + struct.pack("<QQ", len(iw), len(fb)) + iw + fb
@@ -61,23 +68,32 @@ class ResidualBitstream:
     def from_bytes(cls, buf: bytes, device=None) -> "ResidualBitstream":
         fmt = "<4sHHIIIIIII"
         magic, ver, _f, n, C, H, W, h, w, K = struct.unpack_from(fmt, buf, 0)
-        if magic != MAGIC or ver != VERSION:
+        if magic != MAGIC or ver not in (1, VERSION):
             raise ValueError("not an IDF residual bitstream")
         o = struct.calcsize(fmt)
+        src = None
+        if ver >= 2:
+            src = struct.unpack_from("<II", buf, o)
+            o += 8
         li, lf = struct.unpack_from("<QQ", buf, o)
         o += 16
         iw = np.frombuffer(buf, "<i4", li // 4, o).copy()
         o += li
         flow = Bitstream.from_bytes(buf[o:o + lf], device)
         t = torch.from_numpy(iw)
-        return cls(flow, t.to(device) if device else t, n, (C, H, W), (h, w), K)
+        return cls(flow, t.to(device) if device else t, n, (C, H, W), (h, w), K,
+                   None if src is None or tuple(src) == (H, W) else tuple(src))
 
 
 class ResidualCodec:
     """uint8 images <-> ResidualBitstream with a flow model (ConditionalFlows or IDFlows)
-    over Patching(input_size -> model H x W) and a VQ-VAE."""
+    over Patching(input_size -> model H x W) and a VQ-VAE.
 
-    def __init__(self, flows_model, vqvae, input_size):
+    pad = (bottom, right): the dataloader's ReplicationPad2d (trainer.py:62), applied on the
+    device to images of size input_size - pad before coding and cropped off after decoding,
+    so the source image comes back exactly.  Images already of input_size are coded as is."""
+
+    def __init__(self, flows_model, vqvae, input_size, pad=(0, 0)):
         from extenddim import Patching
         self.flows = flows_model
         self.vqvae = vqvae
@@ -85,6 +101,17 @@ class ResidualCodec:
         self.patch = Patching(self.H, self.W, flows_model.H, flows_model.W)
         self.conditional = type(flows_model).__name__ == "ConditionalFlows"
         self.bits = max(1, math.ceil(math.log2(vqvae.embed_num)))
+        self.pad = (int(pad[0]), int(pad[1]))
+
+    @staticmethod
+    def _edge(img_u8, Ho, Wo):
+        B, C, H, W = img_u8.shape
+        if (H, W) == (Ho, Wo):
+            return img_u8
+        out = torch.empty((B, C, Ho, Wo), dtype=torch.uint8, device=img_u8.device)
+        check(lib().idf_pad_edge_u8(_lib.stream_ptr(img_u8.device), B, C, H, W, Ho, Wo,
+                                    ptr(img_u8), ptr(out)), "pad/crop")
+        return out
 
     def _codec(self) -> ImageCodec:
         return self.flows.codec()
@@ -113,8 +140,14 @@ class ResidualCodec:
         if img_u8.dtype != torch.uint8:
             raise TypeError("ResidualCodec.encode expects uint8 images")
         img_u8 = img_u8.contiguous()
+        src_hw = tuple(img_u8.shape[2:])
+        if src_hw == (self.H - self.pad[0], self.W - self.pad[1]):
+            img_u8 = self._edge(img_u8, self.H, self.W)
         B, C, H, W = img_u8.shape
-        assert (H, W) == (self.H, self.W), (H, W)
+        if (H, W) != (self.H, self.W):
+            raise ValueError(f"image size {src_hw}: the codec takes {(self.H, self.W)}"
+                             + (f" or {(self.H - self.pad[0], self.W - self.pad[1])}"
+                                if any(self.pad) else ""))
         data = self._dequant(img_u8)
         idx = self.vqvae.indices(data)                       # [B, h, w] int32
         rec = self.vqvae.reconstruct(idx)                    # NCHW on the grid
@@ -133,7 +166,7 @@ class ResidualCodec:
                                   ptr(words)), "pack idx")
         words = words[:nwd]
         return ResidualBitstream(flow, words, B, (C, H, W), tuple(idx.shape[1:]),
-                                 self.vqvae.embed_num)
+                                 self.vqvae.embed_num, None if src_hw == (H, W) else src_hw)
 
     @torch.no_grad()
     def decode(self, rbs: ResidualBitstream, verify: bool = True):
@@ -163,6 +196,8 @@ class ResidualCodec:
         img = torch.empty((B, C, H, W), dtype=torch.uint8, device=dev)
         bad = torch.zeros(1, dtype=torch.int32, device=dev)
         check(lib().idf_quant_u8(s, B, C, H, W, ptr(pm), 4, ptr(img), ptr(bad)), "quant")
+        if rbs.source_hw:
+            img = self._edge(img, *rbs.source_hw)
         info["off_grid"] = bad
         if verify:
             info["ok"] = bool(info.get("ok", True)) and int(bad.item()) == 0

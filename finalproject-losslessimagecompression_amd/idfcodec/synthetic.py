@@ -61,4 +61,5 @@ def build_residual(name: str, device="cuda", precision: str | None = None):
     flows_model = build_model(configs.get(name)).to(device)
     flows_model.idf_precision = precision or configs.PRECISION.get(name, "f32")
     vq = build_vqvae(vcfg).to(device)
-    return ResidualCodec(flows_model, vq, size), flows_model, vq, size
+    return (ResidualCodec(flows_model, vq, size, configs.PAD.get(name, (0, 0))), flows_model,
+            vq, size)

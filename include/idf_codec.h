@@ -348,6 +348,11 @@ int idf_unpack_bits(void *stream, int64_t groups, int64_t per, int32_t bits,
 /* Patching.forward / backward (extenddim.py:52-67) on NCHW: [B,C,H,W] <-> [B*(H/h)*(W/w),C,h,w]. */
 int idf_patch(void *stream, int32_t B, int32_t C, int32_t H, int32_t W, int32_t h, int32_t w,
               int32_t inverse, const float *d_src, float *d_dst);
+/* trainer.py:62 ReplicationPad2d(padding=(0, Wo-Wi, 0, Ho-Hi)) of uint8 NCHW images
+ * [B,C,Hi,Wi] -> [B,C,Ho,Wo] (Ho >= Hi, Wo >= Wi); with Ho <= Hi, Wo <= Wi the same call is the
+ * top-left crop that undoes it.  Mixed pad/crop is IDF_ERR_ARG. */
+int idf_pad_edge_u8(void *stream, int32_t B, int32_t C, int32_t Hi, int32_t Wi, int32_t Ho,
+                    int32_t Wo, const uint8_t *d_src, uint8_t *d_dst);
 
 #ifdef __cplusplus
 }

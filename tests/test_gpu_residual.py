@@ -1,7 +1,8 @@
 """GPU end-to-end lossless round trips of the residual configs' codec (idfcodec.residual:
 VQ-VAE indices + reconstruction, residual through the flow model over patches, rANS,
 fixed-width index code), on small synthetic models (conditional and plain flows, with and
-without patching) and on the config-3 model (resflow-cond-imagenet64) at full size."""
+without patching) and on the config-3/4/5 models at full size (config 5 from its 215x178
+source through the dataloader's replication pad)."""
 import pytest
 import torch
 
@@ -82,3 +83,57 @@ def test_residual_shards_merge_to_one_bitstream():
     whole = codec.encode(x)
     assert torch.equal(merged.idx_words.cpu(), whole.idx_words.cpu())
     assert torch.equal(merged.flow.states.cpu(), whole.flow.states.cpu())
+
+
+@pytest.mark.parametrize("Hi,Wi,Ho,Wo", [(215, 178, 216, 184), (5, 3, 5, 9), (7, 7, 7, 7),
+                                         (216, 184, 215, 178)])
+def test_pad_edge_matches_replication_pad(Hi, Wi, Ho, Wo):
+    """idf_pad_edge_u8 == nn.ReplicationPad2d((0, right, 0, bottom)) (trainer.py:62) and,
+    shrinking, the crop that undoes it."""
+    from idfcodec import _lib, synthetic
+    from idfcodec._lib import check, lib, ptr
+    x = synthetic.images(2, H=Hi, W=Wi, seed=5).cuda()
+    out = torch.empty((2, 3, Ho, Wo), dtype=torch.uint8, device="cuda")
+    check(lib().idf_pad_edge_u8(_lib.stream_ptr(x.device), 2, 3, Hi, Wi, Ho, Wo, ptr(x), ptr(out)),
+          "pad")
+    if Ho >= Hi:
+        ref = torch.nn.ReplicationPad2d((0, Wo - Wi, 0, Ho - Hi))(x.cpu().float()).to(torch.uint8)
+    else:
+        ref = x.cpu()[:, :, :Ho, :Wo]
+    assert torch.equal(out.cpu(), ref)
+
+
+def test_residual_round_trip_with_source_pad():
+    """A codec with pad=(bottom, right) takes the unpadded source, codes the replication-
+    padded image (what the reference's dataloader hands its trainer) and returns the source."""
+    from idfcodec import synthetic
+    from idfcodec.residual import ResidualBitstream, ResidualCodec
+    fl = _flows("ConditionalFlows", 12, 8, 1, scale=1, conv_for_cond=False)
+    codec = ResidualCodec(fl, _vq_small([8, 16]), (24, 32), pad=(1, 6))
+    x = synthetic.images(2, H=23, W=26, seed=8).cuda()
+    rbs = codec.encode(x)
+    assert rbs.source_hw == (23, 26) and rbs.image_shape == (3, 24, 32)
+    out, info = codec.decode(ResidualBitstream.from_bytes(rbs.to_bytes(), device="cuda"))
+    assert info["ok"] and torch.equal(out, x)
+    padded = torch.nn.ReplicationPad2d((0, 6, 0, 1))(x.cpu().float()).to(torch.uint8).cuda()
+    same = codec.encode(padded)          # the padded image codes to the same streams
+    assert same.source_hw is None and torch.equal(same.idx_words, rbs.idx_words)
+    assert torch.equal(same.flow.words, rbs.flow.words)
+    with pytest.raises(ValueError):
+        codec.encode(synthetic.images(1, H=20, W=20, seed=1).cuda())
+
+
+@pytest.mark.parametrize("name,src", [("resflows_smallpatch_split", (256, 256)),
+                                      ("resflow-patches-vqvae", (215, 178))])
+def test_config45_round_trip_full_size(name, src):
+    """BASELINE configs[3]/[4] at their full model and image sizes, one image each:
+    1024 8x8 patches of a 256x256 image (IDFlows), and 64 27x23 patches of a 215x178 image
+    replication-padded to 216x184 (ConditionalFlows, ExtendDim scale 1)."""
+    from idfcodec import synthetic
+    from idfcodec.residual import ResidualBitstream
+    codec, fl, vq, size = synthetic.build_residual(name)
+    x = synthetic.images(1, H=src[0], W=src[1], seed=6).cuda()
+    rbs = codec.encode(x)
+    assert rbs.image_shape == (3,) + tuple(size) and rbs.index_bits == 13
+    out, info = codec.decode(ResidualBitstream.from_bytes(rbs.to_bytes(), device="cuda"))
+    assert info["ok"] and torch.equal(out, x)

@@ -20,7 +20,11 @@ def close(a, b, tol):
     (3, 32, 32, 52, 44, "ReLU", True), (5, 16, 16, 100, 44, "ReLU", True),
     (7, 8, 8, 168, 44, "ReLU", True), (2, 64, 64, 8, 16, "LeakyReLU", True),
     (4, 4, 4, 24, 32, "ReLU", False), (2, 2, 6, 12, 44, "ReLU", True),
-    (3, 32, 32, 496, 44, "ReLU", True), (1, 16, 16, 520, 44, "ReLU", True)])
+    (3, 32, 32, 496, 44, "ReLU", True), (1, 16, 16, 520, 44, "ReLU", True),
+    # odd sizes (config 5's 27x23 patches): tiled as the next even size, overhang masked
+    (2, 27, 23, 52, 44, "ReLU", True), (3, 5, 7, 24, 32, "LeakyReLU", True),
+    (4, 1, 3, 16, 16, "ReLU", True), (2, 9, 9, 100, 44, "ReLU", False),
+    (1, 45, 37, 20, 44, "ReLU", True)])
 def test_conv3x3_wino_vs_fp64(B, H, W, C, N, act, fold):
     from idfcodec import _lib
     from idfcodec._lib import check, lib, ptr
@@ -65,10 +69,10 @@ def test_conv3x3_wino_vs_fp64(B, H, W, C, N, act, fold):
     assert torch.all(out[:, N:].cpu() == 0), "wrote outside the N output columns"
 
 
-def test_unsupported_geometry_reported():
+def test_geometry_support_reported():
     from idfcodec._lib import lib
-    assert not lib().idf_conv3x3_wino_supported(27, 23)
-    assert lib().idf_conv3x3_wino_supported(8, 8)
+    assert lib().idf_conv3x3_wino_supported(27, 23) and lib().idf_conv3x3_wino_supported(8, 8)
+    assert not lib().idf_conv3x3_wino_supported(0, 5)
 
 
 def test_imagenet64_blocks_on_winograd_path():

@@ -216,6 +216,32 @@ def test_bitstream_container_roundtrip():
         Bitstream.from_bytes(b"XXXX" + raw[4:])
 
 
+def test_residual_container_roundtrip_and_source_size():
+    """IDFR container: index code + flow streams; version 2 carries the pre-pad source size
+    (config 5's 215x178 -> 216x184 ReplicationPad2d), version 1 streams still read."""
+    import struct
+    from idfcodec.codec import Bitstream
+    from idfcodec.residual import ResidualBitstream
+    nw = torch.tensor([2, 0, 1], dtype=torch.int64)
+    st = torch.tensor([5, -7, 2 ** 40], dtype=torch.int64)
+    w = torch.arange(3, dtype=torch.int32)
+    flow = Bitstream(1, [(6, 4, 4), (12, 2, 2), (48, 1, 1)], st, nw, w)
+    idx = torch.tensor([1, -2, 3], dtype=torch.int32)
+    for src in (None, (215, 178)):
+        rbs = ResidualBitstream(flow, idx, 1, (3, 216, 184), (27, 23), 8192, src)
+        r2 = ResidualBitstream.from_bytes(rbs.to_bytes())
+        assert r2.source_hw == src and r2.image_shape == (3, 216, 184) and r2.grid == (27, 23)
+        assert r2.source_shape == (3,) + (src or (216, 184))
+        assert torch.equal(r2.idx_words, idx) and torch.equal(r2.flow.words, w)
+        assert r2.bits() == flow.bits() + 27 * 23 * 13
+    raw = ResidualBitstream(flow, idx, 1, (3, 216, 184), (27, 23), 8192).to_bytes()
+    v1 = raw[:4] + struct.pack("<H", 1) + raw[6:36] + raw[44:]   # drop the v2 size words
+    r1 = ResidualBitstream.from_bytes(v1)
+    assert r1.source_hw is None and torch.equal(r1.idx_words, idx)
+    with pytest.raises(ValueError):
+        ResidualBitstream.from_bytes(b"IDFX" + raw[4:])
+
+
 # ------------------------------------------------------------------ coder chaining (F4)
 def test_coder_decode_fix_roundtrips_with_oracle(golden, oracle, monkeypatch):
     """coder.Encode chains the state across levels; the reference Decode does not

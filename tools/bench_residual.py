@@ -1,4 +1,4 @@
-"""Throughput of the residual configs' codec (BASELINE configs[2..4]) on one GPU.
+"""Throughput of the residual configs' codec (BASELINE configs[2..4]) on one or more GPUs.
 
 Default: resflow-cond-imagenet64 (configs[2]), batch 1024 synthetic 64x64x3 uint8, seeded
 weights (the configs' checkpoints are absent).  One step = ResidualCodec.encode then
@@ -6,9 +6,18 @@ decode of the batch, inputs resident in HBM.  Prints one JSON line: Mpx/s (encod
 the encode / decode split, the VQ-VAE share of each, bits per pixel (flow streams + index
 code) and the exactness of the round trip.  The flow's DenseLayer convs run in the config's
 precision (bf16 MFMA for resflow-cond-imagenet64, as BASELINE configs[2] names; --precision
-overrides).
+overrides).  Config 5's images are generated at their 215x178 source size and go through
+the dataloader's replication pad (trainer.py:62) inside the codec.
+
+Multi-GPU (configs[3]/[4] are 8-GPU configs): launched under torch.distributed.run, each rank
+codes a contiguous slice of the global batch (no data-path collective) and the per-rank
+bitstreams are gathered to rank 0 over RCCL (idfcodec.dist.gather_residual) inside the
+timed encode; every rank then decodes its own shard.  Times are the max over ranks and the
+pixel count is the whole batch (weak scaling when --batch is per rank, the default).
 
   python tools/bench_residual.py [--config NAME] [--batch B] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \\
+      tools/bench_residual.py --config resflows_smallpatch_split
 """
 from __future__ import annotations
 
@@ -22,22 +31,45 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "finalproject-losslessimagecompression_amd"))
 
 import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+# images per GPU: config 3's B=1024 (BASELINE configs[2]); configs 4/5 sized to a few
+# thousand flow patches per GPU (1024 8x8 patches per 256x256 image, 64 27x23 per image)
+DEFAULT_BATCH = {"resflow-cond-imagenet64": 1024, "resflows_smallpatch_split": 8,
+                 "resflow-patches-vqvae": 32}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="resflow-cond-imagenet64")
-    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--precision", default=None, choices=[None, "f32", "bf16"])
     a = ap.parse_args()
-    from idfcodec import synthetic
-    codec, fl, vq, (H, W) = synthetic.build_residual(a.config, precision=a.precision)
-    img = synthetic.images(a.batch, H=H, W=W, seed=2).cuda()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from idfcodec import configs, synthetic
+    from idfcodec.dist import gather_residual
+    codec, fl, vq, (H, W) = synthetic.build_residual(a.config, device=f"cuda:{local}",
+                                                     precision=a.precision)
+    pb, pr = configs.PAD.get(a.config, (0, 0))
+    Hs, Ws = H - pb, W - pr
+    per = a.batch or DEFAULT_BATCH.get(a.config, 8)
+    full = synthetic.images(per * world, H=Hs, W=Ws, seed=2)
+    img = full[rank * per:(rank + 1) * per].cuda()
 
-    def vq_time(B):
-        data = codec._dequant(img[:B])
+    def sync():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    def vq_time():
+        data = codec._dequant(codec._edge(img, H, W))
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         idx = vq.indices(data)
@@ -49,11 +81,15 @@ def main():
 
     for _ in range(a.warmup):
         out, info = codec.decode(codec.encode(img))
-    torch.cuda.synchronize()
+    sync()
     te = td = 0.0
+    merged = None
     for _ in range(a.steps):
+        sync()
         t0 = time.perf_counter()
         rbs = codec.encode(img)
+        if world > 1:
+            merged = gather_residual(rbs)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         out, info = codec.decode(rbs, verify=False)
@@ -62,21 +98,32 @@ def main():
         te += t1 - t0
         td += t2 - t1
     exact = bool(torch.equal(out, img))
-    t_idx, t_rec = vq_time(a.batch)
-    px = a.batch * H * W
-    print(json.dumps({
-        "metric": f"encode+decode Mpixels/s ({a.config}, bit-exact round trip)",
-        "value": round(px * a.steps / (te + td) / 1e6, 4), "unit": "Mpx/s", "n_gpus": 1,
-        "batch": a.batch, "steps": a.steps, "encode_ms": round(te / a.steps * 1e3, 2),
-        "decode_ms": round(td / a.steps * 1e3, 2),
-        "vq_indices_ms": round(t_idx * 1e3, 2), "vq_reconstruct_ms": round(t_rec * 1e3, 2),
-        "bpp": round(3 * rbs.bpd(), 4), "index_bits_share": round(
-            1 - rbs.flow.bits() / rbs.bits(), 4),
-        "round_trip_exact": exact,
-        "dtype": ("bf16 flow convs (f32 accumulate), f32 heads/VQ-VAE/CDF"
-                  if fl.engine().precision == "bf16" else "f32"),
-        "data": "synthetic uint8, seeded weights"}),
-        flush=True)
+    t_idx, t_rec = vq_time()
+    if world > 1:
+        t = torch.tensor([te, td, t_idx, t_rec, 0.0 if exact else 1.0], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        te, td, t_idx, t_rec = (float(v) for v in t[:4])
+        exact = float(t[4]) == 0.0
+    if rank == 0:
+        bs = merged if merged is not None else rbs
+        px = per * world * Hs * Ws
+        print(json.dumps({
+            "metric": f"encode+decode Mpixels/s ({a.config}, bit-exact round trip)",
+            "value": round(px * a.steps / (te + td) / 1e6, 4), "unit": "Mpx/s", "n_gpus": world,
+            "batch_per_gpu": per, "image": [3, Hs, Ws], "coded_image": [3, H, W],
+            "steps": a.steps, "encode_ms": round(te / a.steps * 1e3, 2),
+            "decode_ms": round(td / a.steps * 1e3, 2),
+            "vq_indices_ms": round(t_idx * 1e3, 2), "vq_reconstruct_ms": round(t_rec * 1e3, 2),
+            "bpp": round(3 * bs.bpd(), 4), "index_bits_share": round(
+                1 - bs.flow.bits() / bs.bits(), 4),
+            "round_trip_exact": exact, "scaling": "weak",
+            "dtype": ("bf16 flow convs (f32 accumulate), f32 heads/VQ-VAE/CDF"
+                      if fl.engine().precision == "bf16" else "f32"),
+            "data": "synthetic uint8, seeded weights"}),
+            flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":
