@@ -79,6 +79,10 @@ struct WinoArgs {
 constexpr int kWThreads = 512;
 constexpr int kWMaxHalo = 400;   // halo pixel slots used per stage
 constexpr int kWSlots = 448;     // slots per channel quad of a stage (kWMaxHalo rounded to 64)
+// Small images packed many to a block (config 4's 4x4 / 2x2 levels: 16 or 64 images of
+// 36 or 16 halo pixels) use a 1024-slot stage instead: 2 x 64 KiB of LDS, which costs no
+// occupancy (the kernel is VGPR-limited to one 8-wave block per CU either way).
+constexpr int kWSlotsBig = 1024;
 constexpr int kWMsPitch = 17;    // M staging: floats per (position, tile) row of 16 n
 constexpr uint32_t kWInvalid = 0xFFFFFFF0u;  // buffer offset that always reads 0
 
@@ -122,7 +126,7 @@ __device__ __forceinline__ int colslot(int j, int EH) { return (j & 1) ? EH + (j
 
 // The work of a wave whose positions are (A, 2*BP) and (A, 2*BP + 1): per tile-fragment i
 // (16 tiles) six halo reads, the shared B^T row combination and 2 x NF x 4 MFMAs.
-// xq: this lane's channel quad of a stage's halo image ([4 quads][kWSlots][4 floats]).
+// xq: this lane's channel quad of a stage's halo image ([4 quads][SLOTS][4 floats]).
 template <int NF, int A, int BP>
 struct WinoRole {
   using RA = BT<A>;
@@ -188,11 +192,11 @@ struct WinoRole {
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-template <int NF>
+template <int NF, int SLOTS>
 __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
-  // one stage = the slab's halo image [4 quads][kWSlots][4 floats]
-  constexpr int STAGE = 4 * kWSlots * 4;
-  constexpr int XI_PER_W = (4 * kWSlots / 64 + 7) / 8;  // halo DMA instructions per wave
+  // one stage = the slab's halo image [4 quads][SLOTS][4 floats]
+  constexpr int STAGE = 4 * SLOTS * 4;
+  constexpr int XI_PER_W = (4 * SLOTS / 64 + 7) / 8;  // halo DMA instructions per wave
   constexpr int MS = 16 * 64 * kWMsPitch;  // output-transform staging, aliases the stages
   __shared__ __attribute__((aligned(16))) float lds[2 * STAGE > MS ? 2 * STAGE : MS];
 
@@ -250,7 +254,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
         const int q = f / nblk, k = f - q * nblk;
         const bool ok = x_src[m] != kWInvalid && c0 + 4 * q < g.C;
         const uint32_t off = ok ? x_src[m] + (uint32_t)c0 * 4u : kWInvalid;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_ptr_t)(St + (q * kWSlots + 64 * k) * 4),
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_ptr_t)(St + (q * SLOTS + 64 * k) * 4),
                                                  16, off, 0, 0, 0);
       }
     }
@@ -308,12 +312,12 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
       load_u(s_lo, ucur);
     }
     __syncthreads();  // waits for the DMA (vmcnt) before the barrier
-    if (s_lo < s_hi) role.fetch(lds + lq * kWSlots * 4, tbase[0], d[0]);
+    if (s_lo < s_hi) role.fetch(lds + lq * SLOTS * 4, tbase[0], d[0]);
     for (int s = s_lo; s < s_hi; ++s) {
       const int buf = (s - s_lo) & 1;
       const bool more = s + 1 < s_hi;
-      const float* xq = lds + buf * STAGE + lq * kWSlots * 4;
-      const float* xn = lds + (buf ^ 1) * STAGE + lq * kWSlots * 4;
+      const float* xq = lds + buf * STAGE + lq * SLOTS * 4;
+      const float* xn = lds + (buf ^ 1) * STAGE + lq * SLOTS * 4;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         w4 v0, v1;
@@ -446,7 +450,7 @@ __global__ void __launch_bounds__(256) conv3_wino_reduce_kernel(WinoArgs g) {
 }
 
 struct WinoPlan {
-  int ok, IMGS, TH, TW, ksplit;
+  int ok, IMGS, TH, TW, ksplit, big;
 };
 
 // Output tile and split for an image geometry (never the batch size).  Odd H or W are
@@ -454,7 +458,7 @@ struct WinoPlan {
 // (out-of-image halo) and its outputs are never stored, so every stored pixel sees the
 // same 3x3 neighbourhood as in the direct conv.
 static WinoPlan wino_plan(int H, int W, int nslab) {
-  WinoPlan pl = {0, 1, 0, 0, 1};
+  WinoPlan pl = {0, 1, 0, 0, 1, 0};
   if (H < 1 || W < 1) return pl;
   const int He = (H + 1) & ~1, We = (W + 1) & ~1;
   pl.TW = We < 32 ? We : 32;
@@ -471,8 +475,14 @@ static WinoPlan wino_plan(int H, int W, int nslab) {
     pl.IMGS = 256 / (pl.TH * pl.TW);
     if (pl.IMGS < 1) pl.IMGS = 1;
   }
-  while (pl.IMGS > 1 && pl.IMGS * (pl.TH + 2) * (pl.TW + 2) > kWMaxHalo) --pl.IMGS;
-  if ((pl.TH + 2) * (pl.TW + 2) > kWMaxHalo) return pl;
+  const int want = pl.IMGS, halo = (pl.TH + 2) * (pl.TW + 2);
+  while (pl.IMGS > 1 && pl.IMGS * halo > kWMaxHalo) --pl.IMGS;
+  if (pl.IMGS < want) {  // whole small images: pack up to 64 tiles in the big stage
+    pl.big = 1;
+    pl.IMGS = want;
+    while (pl.IMGS > 1 && pl.IMGS * halo > kWSlotsBig) --pl.IMGS;
+  }
+  if (halo > kWMaxHalo) return pl;
   const int px = H * W;
   pl.ksplit = px <= 64 ? 4 : (px <= 144 ? 2 : 1);
   if (pl.ksplit > nslab) pl.ksplit = nslab > 0 ? nslab : 1;
@@ -530,11 +540,22 @@ extern "C" int idf_conv3x3_wino(void* stream, int32_t B, int32_t H, int32_t W, i
   }
   const int64_t blocks = (int64_t)g.tiles_b * g.tiles_y * g.tiles_x * g.n_tiles * pl.ksplit;
   hipStream_t s = (hipStream_t)stream;
-  switch (NF) {
-    case 1: hipLaunchKernelGGL(conv3_wino_kernel<1>, dim3((unsigned)blocks), dim3(kWThreads), 0, s, g); break;
-    case 2: hipLaunchKernelGGL(conv3_wino_kernel<2>, dim3((unsigned)blocks), dim3(kWThreads), 0, s, g); break;
-    default: hipLaunchKernelGGL(conv3_wino_kernel<3>, dim3((unsigned)blocks), dim3(kWThreads), 0, s, g); break;
+#define IDF_WINO_LAUNCH(nf, slots) \
+  hipLaunchKernelGGL((conv3_wino_kernel<nf, slots>), dim3((unsigned)blocks), dim3(kWThreads), 0, s, g)
+  if (pl.big) {
+    switch (NF) {
+      case 1: IDF_WINO_LAUNCH(1, kWSlotsBig); break;
+      case 2: IDF_WINO_LAUNCH(2, kWSlotsBig); break;
+      default: IDF_WINO_LAUNCH(3, kWSlotsBig); break;
+    }
+  } else {
+    switch (NF) {
+      case 1: IDF_WINO_LAUNCH(1, kWSlots); break;
+      case 2: IDF_WINO_LAUNCH(2, kWSlots); break;
+      default: IDF_WINO_LAUNCH(3, kWSlots); break;
+    }
   }
+#undef IDF_WINO_LAUNCH
   if (pl.ksplit > 1) {
     const int64_t n = (int64_t)B * H * W * N;
     hipLaunchKernelGGL(conv3_wino_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,

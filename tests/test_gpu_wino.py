@@ -24,7 +24,10 @@ def close(a, b, tol):
     # odd sizes (config 5's 27x23 patches): tiled as the next even size, overhang masked
     (2, 27, 23, 52, 44, "ReLU", True), (3, 5, 7, 24, 32, "LeakyReLU", True),
     (4, 1, 3, 16, 16, "ReLU", True), (2, 9, 9, 100, 44, "ReLU", False),
-    (1, 45, 37, 20, 44, "ReLU", True)])
+    (1, 45, 37, 20, 44, "ReLU", True),
+    # many small images per block in the 1024-slot stage (config 4's 4x4 and 2x2 levels)
+    (130, 2, 2, 40, 44, "ReLU", True), (33, 4, 4, 100, 44, "ReLU", True),
+    (17, 3, 3, 24, 32, "LeakyReLU", False)])
 def test_conv3x3_wino_vs_fp64(B, H, W, C, N, act, fold):
     from idfcodec import _lib
     from idfcodec._lib import check, lib, ptr
