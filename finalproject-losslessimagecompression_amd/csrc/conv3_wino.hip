@@ -74,6 +74,8 @@ struct WinoArgs {
   int64_t ldo;
   float* part;
   int32_t ldp;
+  const float* res;  // optional residual added before the activation (VQ-VAE ResBlock)
+  int64_t ldr;
 };
 
 constexpr int kWThreads = 512;
@@ -425,8 +427,11 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
             const int y = y0 + 2 * ty + r, x = x0 + 2 * tx + c;
             if (b >= g.B || y >= g.H || x >= g.Wd) continue;
             const int64_t p = ((int64_t)b * g.H + y) * g.Wd + x;
-            if (g.ksplit == 1)
-              g.out[p * g.ldo + n] = wact(Y[r][c] + wbias(g, n, y, x), g.act, g.slope);
+            if (g.ksplit == 1) {
+              float v = Y[r][c] + wbias(g, n, y, x);
+              if (g.res) v = g.res[p * g.ldr + n] + v;
+              g.out[p * g.ldo + n] = wact(v, g.act, g.slope);
+            }
             else
               g.part[((int64_t)ks * ((int64_t)g.B * g.H * g.Wd) + p) * g.ldp + n] = Y[r][c];
           }
@@ -446,7 +451,9 @@ __global__ void __launch_bounds__(256) conv3_wino_reduce_kernel(WinoArgs g) {
   for (int k = 1; k < g.ksplit; ++k) s = s + g.part[((int64_t)k * P + p) * g.ldp + n];
   const int64_t rem = p % ((int64_t)g.H * g.Wd);
   const int y = (int)(rem / g.Wd), x = (int)(rem % g.Wd);
-  g.out[p * g.ldo + n] = wact(s + wbias(g, n, y, x), g.act, g.slope);
+  float v = s + wbias(g, n, y, x);
+  if (g.res) v = g.res[p * g.ldr + n] + v;
+  g.out[p * g.ldo + n] = wact(v, g.act, g.slope);
 }
 
 struct WinoPlan {
@@ -505,12 +512,11 @@ extern "C" int64_t idf_conv3x3_wino_workspace(int32_t B, int32_t H, int32_t W, i
   return (int64_t)pl.ksplit * B * H * W * ((N + 3) / 4 * 4);
 }
 
-extern "C" int idf_conv3x3_wino(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
-                                const float* x, int64_t ld_x, const float* u, int32_t nft,
-                                const float* b3, const float* vtap, int32_t ldv,
-                                const float* bfull, int32_t N, float* out, int64_t ld_out,
-                                int32_t act, float slope, float* workspace,
-                                int64_t workspace_floats) {
+static int wino_launch(void* stream, int32_t B, int32_t H, int32_t W, int32_t C, const float* x,
+                       int64_t ld_x, const float* u, int32_t nft, const float* b3,
+                       const float* vtap, int32_t ldv, const float* bfull, int32_t N, float* out,
+                       int64_t ld_out, const float* res, int64_t ld_res, int32_t act, float slope,
+                       float* workspace, int64_t workspace_floats) {
   if (B <= 0 || H <= 0 || W <= 0 || N <= 0) return IDF_OK;
   if (C <= 0 || (C & 3) || (ld_x & 3) || !u) return IDF_ERR_ARG;
   const int nf_total = (N + 15) / 16;
@@ -531,7 +537,9 @@ extern "C" int idf_conv3x3_wino(void* stream, int32_t B, int32_t H, int32_t W, i
   if (g.n_tiles * NF > nft) return IDF_ERR_ARG;
   g.b3 = b3; g.vtap = vtap; g.bfull = bfull; g.ldv = ldv; g.act = act; g.slope = slope;
   g.out = out; g.ldo = ld_out;
+  g.res = res; g.ldr = ld_res;
   if (vtap && (!bfull || ldv < N)) return IDF_ERR_ARG;
+  if (res && ld_res < N) return IDF_ERR_ARG;
   if (pl.ksplit > 1) {
     g.ldp = (N + 3) / 4 * 4;
     if (!workspace || workspace_floats < (int64_t)pl.ksplit * B * H * W * g.ldp)
@@ -562,4 +570,23 @@ extern "C" int idf_conv3x3_wino(void* stream, int32_t B, int32_t H, int32_t W, i
                        s, g);
   }
   return idf_last_error();
+}
+
+extern "C" int idf_conv3x3_wino(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
+                                const float* x, int64_t ld_x, const float* u, int32_t nft,
+                                const float* b3, const float* vtap, int32_t ldv,
+                                const float* bfull, int32_t N, float* out, int64_t ld_out,
+                                int32_t act, float slope, float* workspace,
+                                int64_t workspace_floats) {
+  return wino_launch(stream, B, H, W, C, x, ld_x, u, nft, b3, vtap, ldv, bfull, N, out, ld_out,
+                     nullptr, 0, act, slope, workspace, workspace_floats);
+}
+
+extern "C" int idf_conv3x3_wino_res(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
+                                    const float* x, int64_t ld_x, const float* u, int32_t nft,
+                                    const float* bias, int32_t N, float* out, int64_t ld_out,
+                                    const float* res, int64_t ld_res, int32_t act, float slope,
+                                    float* workspace, int64_t workspace_floats) {
+  return wino_launch(stream, B, H, W, C, x, ld_x, u, nft, bias, nullptr, 0, nullptr, N, out,
+                     ld_out, res, ld_res, act, slope, workspace, workspace_floats);
 }

@@ -465,35 +465,6 @@ __global__ void pm_nchw_kernel(int B, int C, int H, int W, const float* __restri
     dst[(b * hw + pix) * ld + c] = src[i];  // here src is NCHW, dst pixel-major
 }
 
-// Conv2d(ci, co, 4, stride 2, pad 1) direct (flows.py:298-301) -- small, cond path only.
-__global__ void conv4x4s2_kernel(int B, int H, int W, int ci, int co, const float* __restrict__ src,
-                                 int64_t lds, const float* __restrict__ w,
-                                 const float* __restrict__ bias, float* __restrict__ dst,
-                                 int64_t ldd) {
-  int Ho = H / 2, Wo = W / 2;
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  int64_t total = (int64_t)B * Ho * Wo * co;
-  if (i >= total) return;
-  int o = (int)(i % co);
-  int64_t op = i / co;
-  int ox = (int)(op % Wo);
-  int64_t t = op / Wo;
-  int oy = (int)(t % Ho);
-  int64_t b = t / Ho;
-  float acc = 0.0f;
-  for (int c = 0; c < ci; ++c)
-    for (int ky = 0; ky < 4; ++ky) {
-      int y = oy * 2 - 1 + ky;
-      if (y < 0 || y >= H) continue;
-      for (int kx = 0; kx < 4; ++kx) {
-        int x = ox * 2 - 1 + kx;
-        if (x < 0 || x >= W) continue;
-        acc = __builtin_fmaf(src[((b * H + y) * W + x) * lds + c], w[((o * ci + c) * 4 + ky) * 4 + kx], acc);
-      }
-    }
-  dst[op * ldd + o] = acc + bias[o];
-}
-
 static inline dim3 grid1d(int64_t n, int bs = 256) { return dim3((unsigned)((n + bs - 1) / bs)); }
 
 }  // namespace idf
@@ -752,16 +723,6 @@ int idf_nchw_to_pm(void* stream, int32_t B, int32_t C, int32_t H, int32_t W, con
   if (n <= 0) return IDF_OK;
   hipLaunchKernelGGL(pm_nchw_kernel, grid1d(n), dim3(256), 0, (hipStream_t)stream, B, C, H, W, src,
                      ld_dst, dst, 0);
-  return idf_last_error();
-}
-
-int idf_conv4x4s2_f32(void* stream, int32_t B, int32_t H, int32_t W, int32_t ci, int32_t co,
-                      const float* src, int64_t ld_src, const float* w, const float* bias,
-                      float* dst, int64_t ld_dst) {
-  int64_t n = (int64_t)B * (H / 2) * (W / 2) * co;
-  if (n <= 0) return IDF_OK;
-  hipLaunchKernelGGL(conv4x4s2_kernel, grid1d(n), dim3(256), 0, (hipStream_t)stream, B, H, W, ci,
-                     co, src, ld_src, w, bias, dst, ld_dst);
   return idf_last_error();
 }
 

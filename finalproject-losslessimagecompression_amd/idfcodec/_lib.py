@@ -97,6 +97,8 @@ SIGNATURES = {
     "idf_conv3x3_wino_workspace": (i64, [i32, i32, i32, i32, i32]),
     "idf_conv3x3_wino": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, P, P, i32, P, i32, P,
                                         i64, i32, f32, P, i64]),
+    "idf_conv3x3_wino_res": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, P, i32, P, i64,
+                                            P, i64, i32, f32, P, i64]),
     "idf_conv3x3_bf16_workspace": (i64, [i32, i32, i32, i32, i32]),
     "idf_conv3x3_bf16": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, P, P, i32, P, i32, P,
                                         i64, i32, f32, P, i64]),
@@ -108,7 +110,6 @@ SIGNATURES = {
     "idf_copy_cols": (ctypes.c_int, [P, i64, i32, i32, P, i64, P, i64]),
     "idf_pm_to_nchw": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P]),
     "idf_nchw_to_pm": (ctypes.c_int, [P, i32, i32, i32, i32, P, P, i64]),
-    "idf_conv4x4s2_f32": (ctypes.c_int, [P, i32, i32, i32, i32, i32, P, i64, P, P, P, i64]),
     "idf_conv_taps_n_alloc": (ctypes.c_int, [i32]),
     "idf_conv_taps_f32": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, i32, i32, i32, i32, i32, P,
                                          P, P, i32, i32, P, i32, P, i64, i32, i32, i32, i32, i32,

@@ -219,10 +219,13 @@ class FlowEngine:
             self.ids.append(ids_l)
             self.inv_ids.append(inv_l)
         if self.conv_for_cond:
-            self.cond_w = [sd[f"convs.{l}.weight"].detach().float().contiguous().to(self.device)
-                           for l in range(self.nsplit)]
-            self.cond_b = [sd[f"convs.{l}.bias"].detach().float().contiguous().to(self.device)
-                           for l in range(self.nsplit)]
+            # Conv2d(c, 4c, 4, 2, 1) (flows.py:298-301) as an implicit GEMM on the MFMA tap
+            # kernel shared with the VQ-VAE (vq_kernels.hip conv_taps_kernel)
+            from .vq import DevConv, pack_conv
+            self.cond_conv = [DevConv(pack_conv(sd[f"convs.{l}.weight"].detach().double().cpu(),
+                                                sd[f"convs.{l}.bias"].detach().double().cpu(),
+                                                stride=2, padding=1), self.device)
+                              for l in range(self.nsplit)]
         blocks = [b for lv in self.couple for b in lv] + self.prior
         self.ld_feat = max(b.geom.ld_feat for b in blocks)
         self._ws = {}
@@ -269,7 +272,8 @@ class FlowEngine:
         }
         if self.conditional:
             ws["cond"] = [f(B * L.h * L.w * round_up(L.cond_ch, 4)) for L in self.levels]
-            ws["cond_img"] = f(B * self.H * self.W * 4)
+            # channels C..3 of the 4-wide pixel rows stay zero (they meet zero weights)
+            ws["cond_img"] = torch.zeros(B * self.H * self.W * 4, dtype=torch.float32, device=dev)
         self._ws = {B: ws}  # keep one batch size resident
         return ws
 
@@ -290,9 +294,13 @@ class FlowEngine:
         for l, Lv in enumerate(self.levels):
             dst, ldd = ws["cond"][l], round_up(Lv.cond_ch, 4)
             if self.conv_for_cond:
-                check(L.idf_conv4x4s2_f32(s, B, H, W, C, Lv.cond_ch, ptr(src), ld,
-                                          ptr(self.cond_w[l]), ptr(self.cond_b[l]), ptr(dst), ldd),
-                      "conv4x4s2")
+                dc = self.cond_conv[l]
+                c = dc.c
+                check(L.idf_conv_taps_f32(s, B, H, W, round_up(C, 4), ptr(src), ld, H // 2, W // 2,
+                                          2, 2, len(c.dy), dc.dy, dc.dx, ptr(dc.w), c.ldw,
+                                          c.n_alloc, ptr(dc.b), Lv.cond_ch, ptr(dst), ldd, H // 2,
+                                          W // 2, 1, 1, 0, 0, None, 0, _lib.ACT["None"], 0.0),
+                      "cond conv")
             else:
                 check(L.idf_squeeze(s, B, H, W, C, self.scale, ptr(src), ld, ptr(dst), ldd),
                       "squeeze")

@@ -2,7 +2,9 @@
 
 Every convolution is one `idf_conv_taps_f32` launch over a tap table (csrc/vq_kernels.hip):
 Conv2d(k, s, p) is Hc = Ho, isy = s, taps (ky - p, kx - p); ConvTranspose2d(4, 2, 1) is four
-launches, one per output parity (py, px), each a 2x2-tap conv on the input grid.  Activations
+launches, one per output parity (py, px), each a 2x2-tap conv on the input grid.  The 3x3
+stride-1 convs (ResBlocks: 80-85% of the VQ-VAE's FLOPs) run as Winograd F(2x2, 3x3) instead
+(`idf_conv3x3_wino_res`, csrc/conv3_wino.hip, residual add fused before the activation).  Activations
 are pixel-major with channel pitch round_up(C, 4); the 3-channel image is padded to 4 with
 zeros (zero weights).  The batch_norm=True variants (BatchNorm after the activation,
 vqvae.py:31-35) are rejected: no north-star config uses them.
@@ -169,10 +171,21 @@ def decoder_stages(dec) -> list[Stage]:
     return [_seq_conv(b) if isinstance(b, nn.Sequential) else _res_stage(b) for b in dec.blocks]
 
 
+def is_wino(c: TapConv) -> bool:
+    """Conv2d(k=3, s=1, p=1) with channel counts the Winograd kernel takes."""
+    return (len(c.dy) == 9 and c.isy == 1 and c.osy == 1 and c.cin % 4 == 0
+            and list(zip(c.dy, c.dx)) == [(y, x) for y in (-1, 0, 1) for x in (-1, 0, 1)])
+
+
 class DevConv:
-    def __init__(self, c: TapConv, device):
+    def __init__(self, c: TapConv, device, wino: bool = True):
         self.c = c
         self.w = torch.from_numpy(c.w).to(device)
+        self.wino_u = None
+        if wino and is_wino(c):
+            from .packing import wino_weights
+            self.wino_u = torch.from_numpy(
+                wino_weights(c.w.astype(np.float64), c.ldw // 16)).to(device)
         self.b = torch.from_numpy(c.bias).to(device)
         self.dy = (ctypes.c_int32 * len(c.dy))(*c.dy)
         self.dx = (ctypes.c_int32 * len(c.dx))(*c.dx)
@@ -181,8 +194,10 @@ class DevConv:
 class VQEngine:
     """Device VQ-VAE: indices and reconstruction of a batch of images."""
 
-    def __init__(self, model, device):
+    def __init__(self, model, device, wino: bool = True):
         self.device = device
+        self.wino = wino
+        self._ws = None
         self.channel = model.channel
         self.D = model.embed_dim
         self.K = model.embed_num
@@ -194,11 +209,20 @@ class VQEngine:
                                  ptr(self.enorm)), "vq norms")
 
     def _dev(self, st: Stage):
-        return (st, [DevConv(c, self.device) for c in st.convs])
+        return (st, [DevConv(c, self.device, self.wino) for c in st.convs])
 
     # ---------------------------------------------------------------- conv runner
     def _conv(self, s, dc: DevConv, x, B, H, W, ldx, act, out, ldo, Ho, Wo, res=None, ldr=0):
         c = dc.c
+        if dc.wino_u is not None:
+            L = lib()
+            wsn = int(L.idf_conv3x3_wino_workspace(B, H, W, c.cin, c.cout))
+            ws = self._wino_ws(wsn)
+            check(L.idf_conv3x3_wino_res(
+                s, B, H, W, c.cin, ptr(x), ldx, ptr(dc.wino_u), c.n_alloc // 16, ptr(dc.b), c.cout,
+                ptr(out), ldo, ptr(res) if res is not None else None, ldr, act, LEAKY,
+                ptr(ws) if wsn else None, wsn), "vq wino conv")
+            return
         if c.osy == 2:      # transposed: compute grid = input grid
             Hc, Wc = H, W
         else:
@@ -208,6 +232,11 @@ class VQEngine:
             dc.dx, ptr(dc.w), c.ldw, c.n_alloc, ptr(dc.b), c.cout, ptr(out), ldo, Ho, Wo, c.osy,
             c.osy, c.oy0, c.ox0, ptr(res) if res is not None else None, ldr, act, LEAKY),
             "vq conv")
+
+    def _wino_ws(self, n):
+        if n and (self._ws is None or self._ws.numel() < n):
+            self._ws = torch.empty(n, dtype=torch.float32, device=self.device)
+        return self._ws
 
     def _run(self, stages, x, B, H, W, C):
         """Run conv stages on a pixel-major buffer x [B*H*W][round_up(C,4)]."""

@@ -251,7 +251,8 @@ int idf_conv3x3_halo(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, c
 /* The same 3x3 conv as Winograd F(2x2, 3x3): 16 multiplies per 2x2 outputs instead
  * of 36.  d_u holds U = G g G^T per (position, n, c), pre-arranged in MFMA fragment
  * order [16 positions][ceil(C/16) slabs][nft n-fragments][64 lanes][4]
- * (idfcodec/packing.py wino_weights).  Even H and W only (else IDF_ERR_UNSUPPORTED). */
+ * (idfcodec/packing.py wino_weights).  Any H, W >= 1 (odd sizes are tiled as the next
+ * even size; the overhang reads zero padding and is never stored). */
 int idf_conv3x3_wino_supported(int32_t H, int32_t W);
 int64_t idf_conv3x3_wino_workspace(int32_t B, int32_t H, int32_t W, int32_t C, int32_t N);
 int idf_conv3x3_wino(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, const float *d_x,
@@ -259,6 +260,14 @@ int idf_conv3x3_wino(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, c
                      const float *d_vtap, int32_t ldv, const float *d_bfull, int32_t N,
                      float *d_out, int64_t ld_out, int32_t act, float slope, float *d_workspace,
                      int64_t workspace_floats);
+/* The same Winograd conv as a plain Conv2d(C, N, 3, padding=1) with bias and an optional
+ * residual (NULL for none): out = act(res + (conv(x) + bias)) -- the VQ-VAE's 3x3 convs and
+ * ResBlocks (nnblock.py:59-84, vqvae.py:22-113).  Same workspace rule as idf_conv3x3_wino. */
+int idf_conv3x3_wino_res(void *stream, int32_t B, int32_t H, int32_t W, int32_t C,
+                         const float *d_x, int64_t ld_x, const float *d_u, int32_t nft,
+                         const float *d_bias, int32_t N, float *d_out, int64_t ld_out,
+                         const float *d_res, int64_t ld_res, int32_t act, float slope,
+                         float *d_workspace, int64_t workspace_floats);
 
 /* The same folded 3x3 conv on bf16 MFMA (v_mfma_f32_16x16x32_bf16, fp32 accumulation): X is
  * read as fp32 and rounded to bf16 (nearest even) on its way into LDS; d_wb holds the
@@ -301,11 +310,6 @@ int idf_pm_to_nchw(void *stream, int32_t B, int32_t C, int32_t H, int32_t W, con
                    int64_t ld_src, float *d_dst);
 int idf_nchw_to_pm(void *stream, int32_t B, int32_t C, int32_t H, int32_t W, const float *d_src,
                    float *d_dst, int64_t ld_dst);
-/* ConditionalFlows cond conv (flows.py:298-301): Conv2d(ci, co, 4, stride 2, pad 1) on
- * pixel-major input [B,H,W,ci] -> [B,H/2,W/2,co]; w in PyTorch layout [co][ci][4][4]. */
-int idf_conv4x4s2_f32(void *stream, int32_t B, int32_t H, int32_t W, int32_t ci, int32_t co,
-                      const float *d_src, int64_t ld_src, const float *d_w, const float *d_bias,
-                      float *d_dst, int64_t ld_dst);
 
 /* ======================================================================== *
  * VQ-VAE of the residual configs (vqvae.py:22-168; configs 3-5), pixel-major fp32.

@@ -113,3 +113,43 @@ def test_imagenet64_blocks_on_winograd_path():
                                     None), "head")
         got = out[:, :n].view(2, hw, hw, n).permute(0, 3, 1, 2)
         close(got, ref, 1e-5)
+
+
+@pytest.mark.parametrize("B,H,W,C,N,act,res", [
+    (4, 8, 8, 384, 384, "ReLU", True),      # config 3 ResBlock conv2 (8x8 latents)
+    (2, 8, 8, 384, 384, "ReLU", False),     # ResBlock conv1
+    (1, 32, 32, 64, 64, "ReLU", True), (3, 7, 5, 16, 20, "None", True)])
+def test_conv3x3_wino_res_vs_fp64(B, H, W, C, N, act, res):
+    """idf_conv3x3_wino_res (the VQ-VAE's 3x3 convs): act(res + conv3x3(x) + bias)."""
+    from idfcodec import _lib
+    from idfcodec._lib import check, lib, ptr
+    from idfcodec.packing import round_up, wino_weights
+    g = torch.Generator().manual_seed(B + H * 5 + C)
+    ld = round_up(C, 4)
+    ldo = round_up(N, 4)
+    X = torch.randn(B * H * W, ld, generator=g)
+    R = torch.randn(B * H * W, ldo, generator=g)
+    ldw = round_up(C, 16)
+    n_alloc = round_up(N, 16)
+    Wt = torch.randn(n_alloc, 9, ldw, generator=g, dtype=torch.float64) / np.sqrt(9 * C)
+    bias = torch.randn(n_alloc, generator=g) * 0.1
+    dev = torch.device("cuda")
+    Ud = torch.from_numpy(wino_weights(Wt.numpy(), ldw // 16)).to(dev)
+    Xd, Rd, bd = X.to(dev), R.to(dev), bias.to(dev)
+    out = torch.zeros(B * H * W, ldo, device=dev)
+    wsn = lib().idf_conv3x3_wino_workspace(B, H, W, C, N)
+    ws = torch.empty(max(wsn, 1), device=dev)
+    check(lib().idf_conv3x3_wino_res(_lib.stream_ptr(), B, H, W, C, ptr(Xd), ld, ptr(Ud),
+                                     n_alloc // 16, ptr(bd), N, ptr(out), ldo,
+                                     ptr(Rd) if res else None, ldo, _lib.ACT[act], 0.01, ptr(ws),
+                                     wsn), "wino_res")
+    torch.cuda.synchronize()
+    x4 = X[:, :C].double().view(B, H, W, C).permute(0, 3, 1, 2)
+    w4 = Wt[:N, :, :C].permute(0, 2, 1).reshape(N, C, 3, 3)
+    ref = F.conv2d(x4, w4, padding=1) + bias[:N].double().view(1, -1, 1, 1)
+    if res:
+        ref = ref + R[:, :N].double().view(B, H, W, N).permute(0, 3, 1, 2)
+    if act == "ReLU":
+        ref = F.relu(ref)
+    got = out[:, :N].cpu().double().view(B, H, W, N).permute(0, 3, 1, 2)
+    close(got, ref, 1e-5)
