@@ -200,7 +200,8 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   constexpr int STAGE = 4 * SLOTS * 4;
   constexpr int XI_PER_W = (4 * SLOTS / 64 + 7) / 8;  // halo DMA instructions per wave
   constexpr int MS = 16 * 64 * kWMsPitch;  // output-transform staging, aliases the stages
-  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE > MS ? 2 * STAGE : MS];
+  constexpr int BT = 16 * NF * 16;         // epilogue bias table, after the staging
+  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE > MS + BT ? 2 * STAGE : MS + BT];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -379,6 +380,8 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
 
   // ---- output transform, one n-fragment at a time through LDS
   float* Ms = lds;  // [16 pos][64 tiles][kWMsPitch]
+  float* btab = lds + MS;  // [16 border classes][NF * 16]
+  if (g.ksplit == 1) stage_bias(btab, NF * 16, nf0 * 16, g.N, g.b3, g.vtap, g.bfull, g.ldv, tid, kWThreads);
 #pragma unroll
   for (int j = 0; j < NF; ++j) {
 #pragma unroll
@@ -428,7 +431,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
             if (b >= g.B || y >= g.H || x >= g.Wd) continue;
             const int64_t p = ((int64_t)b * g.H + y) * g.Wd + x;
             if (g.ksplit == 1) {
-              float v = Y[r][c] + wbias(g, n, y, x);
+              float v = Y[r][c] + btab[bias_class(y, x, g.H, g.Wd) * (NF * 16) + n - nf0 * 16];
               if (g.res) v = g.res[p * g.ldr + n] + v;
               g.out[p * g.ldo + n] = wact(v, g.act, g.slope);
             }

@@ -542,18 +542,40 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
   const int64_t P = (int64_t)B * H * W;
   if (ld_feat < blk->k_in[blk->depth] || ld_tmp < blk->k_in[blk->depth]) return IDF_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
+  // bf16 blocks keep a bf16 shadow of the feature columns at the front of tmp (each layer
+  // writes its output in both precisions; conv3_bf16.hip DMAs its halos from the shadow),
+  // followed by the split-K partials
+  uint16_t* f16 = nullptr;
+  int64_t ld16 = 0;
+  float* ws = tmp;
+  int64_t ws_floats = P * ld_tmp;
+  if (blk->bf16) {
+    if (!blk->fold) return IDF_ERR_ARG;
+    for (int i = 0; i < blk->depth; ++i)
+      if (!blk->wb16[i]) return IDF_ERR_ARG;
+    ld16 = ((int64_t)blk->k_in[blk->depth] + 7) / 8 * 8;
+    const int64_t sh = (P * ld16 / 2 + 3) / 4 * 4;  // floats
+    if (sh > ws_floats) return IDF_ERR_WORKSPACE;
+    f16 = (uint16_t*)tmp;
+    ws = tmp + sh;
+    ws_floats -= sh;
+    const int c0 = blk->k_in[0];
+    int rc = idf_f32_to_bf16_cols(stream, P, c0, (c0 + 7) / 8 * 8, feat, ld_feat, f16, ld16);
+    if (rc) return rc;
+  }
   for (int i = 0; i < blk->depth; ++i) {
     const int c = blk->k_in[i];
     const double cr = blk->c_real[i], gr = blk->g_real[i];
     if (blk->fold) {  // one launch per layer: 3x3 over the layer input, 1x1 folded in
       timer_mark(timer, s, IDF_TAG_CONV3X3, 2.0 * P * 9.0 * cr * gr, true);
       const bool wino = blk->wino && blk->wino_u[i] && idf_conv3x3_wino_supported(H, W);
-      const bool bf = blk->bf16 && blk->wb16[i];
+      const bool bf = blk->bf16 != 0;
+      const int n16 = (c + blk->g_pad + 7) / 8 * 8 - c;
       int rc = bf
-                   ? idf_conv3x3_bf16(stream, B, H, W, c, feat, ld_feat, blk->wb16[i],
-                                      blk->g_alloc, blk->b3[i], blk->vtap[i], blk->ldv,
-                                      blk->bfull[i], blk->g_pad, feat + c, ld_feat, blk->act,
-                                      blk->slope, tmp, P * ld_tmp)
+                   ? idf_conv3x3_bf16(stream, B, H, W, c, f16, ld16, blk->wb16[i], blk->g_alloc,
+                                      blk->b3[i], blk->vtap[i], blk->ldv, blk->bfull[i],
+                                      blk->g_pad, feat + c, ld_feat, f16 + c, ld16, n16,
+                                      blk->act, blk->slope, ws, ws_floats)
                : wino
                    ? idf_conv3x3_wino(stream, B, H, W, c, feat, ld_feat, blk->wino_u[i],
                                       blk->wino_nft, blk->b3[i], blk->vtap[i], blk->ldv,

@@ -12,3 +12,44 @@ static inline int idf_last_error() {
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? IDF_OK : IDF_ERR_HIP;
 }
+
+namespace idf {
+
+// Border class of an output pixel for the folded 1x1 bias: bit 0 y == 0, bit 1 y == H-1,
+// bit 2 x == 0, bit 3 x == W-1 (class 0 = interior).
+__device__ __forceinline__ int bias_class(int y, int x, int H, int W) {
+  return (y == 0) | ((y == H - 1) << 1) | ((x == 0) << 2) | ((x == W - 1) << 3);
+}
+
+// Stage the epilogue's bias table in LDS: tab[cls * nn + k] for output column n0 + k (k < nn)
+// = b3 (no fold), bfull (interior) or b3 + the vtap of every in-image tap, summed in tap
+// order -- the same values, bit for bit, as evaluating the bias per pixel.  Reading the
+// table from LDS keeps the epilogue's global stores free of (possibly aliasing) global bias
+// loads, which the compiler would otherwise serialise one round trip per store.
+__device__ __forceinline__ void stage_bias(float* tab, int nn, int n0, int N, const float* b3,
+                                           const float* vtap, const float* bfull, int ldv,
+                                           int tid, int nthreads) {
+  for (int e = tid; e < 16 * nn; e += nthreads) {
+    const int cls = e / nn, k = e - cls * nn, n = n0 + k;
+    float v = 0.0f;
+    if (n < N) {
+      if (!vtap) {
+        v = b3[n];
+      } else if (cls == 0) {
+        v = bfull[n];
+      } else {
+        v = b3[n];
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+          const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+          const bool ok = !((dy < 0 && (cls & 1)) || (dy > 0 && (cls & 2)) ||
+                            (dx < 0 && (cls & 4)) || (dx > 0 && (cls & 8)));
+          if (ok) v = v + vtap[tap * ldv + n];
+        }
+      }
+    }
+    tab[e] = v;
+  }
+}
+
+}  // namespace idf

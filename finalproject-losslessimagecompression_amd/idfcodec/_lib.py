@@ -100,8 +100,9 @@ SIGNATURES = {
     "idf_conv3x3_wino_res": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, P, i32, P, i64,
                                             P, i64, i32, f32, P, i64]),
     "idf_conv3x3_bf16_workspace": (i64, [i32, i32, i32, i32, i32]),
-    "idf_conv3x3_bf16": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, P, P, i32, P, i32, P,
-                                        i64, i32, f32, P, i64]),
+    "idf_conv3x3_bf16": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, P, P, i32, P, i32,
+                                        P, i64, P, i64, i32, i32, f32, P, i64]),
+    "idf_f32_to_bf16_cols": (ctypes.c_int, [P, i64, i32, i32, P, i64, P, i64]),
     "idf_dequant_u8": (ctypes.c_int, [P, i32, i32, i32, i32, P, P, i64]),
     "idf_quant_u8": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, P]),
     "idf_squeeze": (ctypes.c_int, [P, i32, i32, i32, i32, i32, P, i64, P, i64]),

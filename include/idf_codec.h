@@ -269,17 +269,26 @@ int idf_conv3x3_wino_res(void *stream, int32_t B, int32_t H, int32_t W, int32_t 
                          const float *d_res, int64_t ld_res, int32_t act, float slope,
                          float *d_workspace, int64_t workspace_floats);
 
-/* The same folded 3x3 conv on bf16 MFMA (v_mfma_f32_16x16x32_bf16, fp32 accumulation): X is
- * read as fp32 and rounded to bf16 (nearest even) on its way into LDS; d_wb holds the
- * weights rounded to bf16 in fragment order [ceil(C/32)][9][4][n_alloc][8]
- * (idfcodec/packing.py bf16_weights), n_alloc = 16*ceil(N/16) <= 48.  For the configs that
- * name bf16 coupling convs (resflow-cond-imagenet64); deterministic and batch-invariant. */
+/* The same folded 3x3 conv on bf16 MFMA (v_mfma_f32_16x16x32_bf16, fp32 accumulation).
+ * The input is the bf16 shadow d_x16 of the fp32 feature columns (ld_x16 a multiple of 8,
+ * 16-B aligned; channels [C, round_up(C, 8)) must hold zeros) -- halos are DMA'd straight
+ * into LDS.  The activated output goes to d_out (fp32) and, rounded to bf16 (nearest even),
+ * to d_out16; columns [N, n16) of d_out16 are zeroed (N <= n16 <= N + 15), so the next
+ * layer's input meets the shadow's zero rule.  d_wb holds the weights rounded to bf16 in
+ * fragment order [ceil(C/32)][9][4][n_alloc][8] (idfcodec/packing.py bf16_weights),
+ * n_alloc = 16*ceil(N/16) <= 48.  For the configs that name bf16 coupling convs
+ * (resflow-cond-imagenet64); deterministic and batch-invariant. */
 int64_t idf_conv3x3_bf16_workspace(int32_t B, int32_t H, int32_t W, int32_t C, int32_t N);
-int idf_conv3x3_bf16(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, const float *d_x,
-                     int64_t ld_x, const uint16_t *d_wb, int32_t n_alloc, const float *d_b3,
-                     const float *d_vtap, int32_t ldv, const float *d_bfull, int32_t N,
-                     float *d_out, int64_t ld_out, int32_t act, float slope, float *d_workspace,
-                     int64_t workspace_floats);
+int idf_conv3x3_bf16(void *stream, int32_t B, int32_t H, int32_t W, int32_t C,
+                     const uint16_t *d_x16, int64_t ld_x16, const uint16_t *d_wb, int32_t n_alloc,
+                     const float *d_b3, const float *d_vtap, int32_t ldv, const float *d_bfull,
+                     int32_t N, float *d_out, int64_t ld_out, uint16_t *d_out16,
+                     int64_t ld_out16, int32_t n16, int32_t act, float slope,
+                     float *d_workspace, int64_t workspace_floats);
+/* dst[p, c] = bf16(src[p, c]) (nearest even) for c < n, 0 for n <= c < n_zero: the bf16
+ * shadow of a DenseBlock's input columns. */
+int idf_f32_to_bf16_cols(void *stream, int64_t P, int32_t n, int32_t n_zero, const float *d_src,
+                         int64_t ld_src, uint16_t *d_dst, int64_t ld_dst);
 
 /* ---- index maps (exact copies; no arithmetic) ---------------------------- */
 /* trainer.py:101 dequant of uint8 NCHW images to the 1/256 grid, written pixel-major:

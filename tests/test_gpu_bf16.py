@@ -21,13 +21,28 @@ def _run(X, Wt, b3, vt, bfull, B, H, W, C, N, act="ReLU"):
     Xd, b3d = X.to(dev), b3.to(dev)
     vtd = vt.to(dev) if vt is not None else None
     bfd = bfull.to(dev) if bfull is not None else None
-    out = torch.zeros(B * H * W, ld, device=dev)
+    P = B * H * W
+    out = torch.zeros(P, ld, device=dev)
+    # bf16 shadow of the input columns (zeros to the next multiple of 8), output columns
+    # at C (the DenseBlock layout), poisoned so unwritten shadow columns show up
+    ld16 = round_up(C + N + 8, 8)
+    x16 = torch.full((P, ld16), 0x7FC0, dtype=torch.int16, device=dev)
+    check(lib().idf_f32_to_bf16_cols(_lib.stream_ptr(), P, C, round_up(C, 8), ptr(Xd), ld,
+                                     ptr(x16), ld16), "to bf16")
+    n16 = round_up(C + N, 8) - C
     wsn = lib().idf_conv3x3_bf16_workspace(B, H, W, C, N)
     ws = torch.empty(max(wsn, 1), device=dev)
-    check(lib().idf_conv3x3_bf16(_lib.stream_ptr(), B, H, W, C, ptr(Xd), ld, ptr(wb), n_alloc,
+    check(lib().idf_conv3x3_bf16(_lib.stream_ptr(), B, H, W, C, ptr(x16), ld16, ptr(wb), n_alloc,
                                  ptr(b3d), ptr(vtd), n_alloc, ptr(bfd), N, ptr(out), ld,
-                                 _lib.ACT[act], 0.01, ptr(ws), wsn), "bf16 conv")
+                                 ptr(x16) + 2 * C, ld16, n16, _lib.ACT[act], 0.01, ptr(ws), wsn),
+          "bf16 conv")
     torch.cuda.synchronize()
+    # the shadow holds bf16(out) for the N output columns and zeros up to n16
+    sh = x16[:, C:C + n16].cpu()
+    want = out[:, :N].cpu().to(torch.bfloat16).view(torch.int16)
+    assert torch.equal(sh[:, :N], want), "bf16 shadow of the output differs"
+    assert torch.all(sh[:, N:] == 0), "shadow pad columns not zeroed"
+    assert torch.all(x16[:, C + n16:].cpu() == 0x7FC0), "wrote past the shadow columns"
     return out.cpu()
 
 

@@ -78,10 +78,15 @@ def main():
             bwn = lib().idf_conv3x3_bf16_workspace(B, hw, hw, c_pad, g_pad)
             bws = torch.empty(max(bwn, 1), device=dev)
 
+            ld16 = (ld + 7) // 8 * 8
+            f16 = torch.zeros(P * ld16, dtype=torch.int16, device=dev)
+            n16 = (c_pad + g_pad + 7) // 8 * 8 - c_pad
+
             def bf16():
-                check(lib().idf_conv3x3_bf16(s, B, hw, hw, c_pad, ptr(feat), ld, ptr(WB), g_alloc,
+                check(lib().idf_conv3x3_bf16(s, B, hw, hw, c_pad, ptr(f16), ld16, ptr(WB), g_alloc,
                                              ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
-                                             ptr(feat) + c_pad * 4, ld, 0, 0.0, ptr(bws), bwn), "bf16")
+                                             ptr(feat) + c_pad * 4, ld, ptr(f16) + c_pad * 2, ld16,
+                                             n16, 0, 0.0, ptr(bws), bwn), "bf16")
 
             def gemm():
                 check(lib().idf_conv3x3_fold_f32(s, B, hw, hw, c_pad, ptr(feat), ld, ptr(w), ldw,
