@@ -33,19 +33,21 @@ __device__ __forceinline__ void stage_bias(float* tab, int nn, int n0, int N, co
     const int cls = e / nn, k = e - cls * nn, n = n0 + k;
     float v = 0.0f;
     if (n < N) {
-      if (!vtap) {
-        v = b3[n];
-      } else if (cls == 0) {
-        v = bfull[n];
-      } else {
-        v = b3[n];
+      // every load unconditional and issued together (one round trip), then combined
+      v = b3[n];
+      if (vtap) {
+        float t[9];
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) t[tap] = vtap[tap * ldv + n];
+        const float full = bfull[n];
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
           const int dy = tap / 3 - 1, dx = tap % 3 - 1;
           const bool ok = !((dy < 0 && (cls & 1)) || (dy > 0 && (cls & 2)) ||
                             (dx < 0 && (cls & 4)) || (dx > 0 && (cls & 8)));
-          if (ok) v = v + vtap[tap * ldv + n];
+          v = ok ? v + t[tap] : v;
         }
+        v = cls == 0 ? full : v;
       }
     }
     tab[e] = v;
