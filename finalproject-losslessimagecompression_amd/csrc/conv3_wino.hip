@@ -45,7 +45,8 @@
 #define IDF_WINO_ABLATE 0
 #endif
 // Where the next slab's loads are issued: 0 = halo DMA + U after group 0's MFMAs,
-// 1 = halo after group 0, U after group 1, 2 = halo pieces between group 1's k-steps.
+// 1 = halo after group 0, U after group 1, 2 = halo pieces between group 1's k-steps,
+// 3 = the halo two slabs ahead, pieces between group 3's k-steps (U after group 1).
 #ifndef IDF_WINO_SCHED
 #define IDF_WINO_SCHED 2
 #endif
@@ -313,6 +314,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
     if (s_lo < s_hi) {
       issue(s_lo, 0);
       load_u(s_lo, ucur);
+      if (IDF_WINO_SCHED == 3 && s_lo + 1 < s_hi) issue(s_lo + 1, 1);
     }
     __syncthreads();  // waits for the DMA (vmcnt) before the barrier
     if (s_lo < s_hi) role.fetch(lds + lq * SLOTS * 4, tbase[0], d[0]);
@@ -333,6 +335,11 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
           role.mfma(v0, v1, ucur, acc[i], [&](int t) {
             if (more && !(IDF_WINO_ABLATE & 1) && t < XI_PER_W) issue_piece(s + 1, buf ^ 1, t);
           });
+        } else if (IDF_WINO_SCHED == 3 && i == 3) {
+          // two slabs ahead: stage buf is free once this slab's barrier (after g2) passed
+          role.mfma(v0, v1, ucur, acc[i], [&](int t) {
+            if (s + 2 < s_hi && !(IDF_WINO_ABLATE & 1) && t < XI_PER_W) issue_piece(s + 2, buf, t);
+          });
         } else {
           role.mfma(v0, v1, ucur, acc[i], [](int) {});
         }
@@ -352,6 +359,11 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
               if (!(IDF_WINO_ABLATE & 1)) issue_piece(s + 1, buf ^ 1, m);
             if (!(IDF_WINO_ABLATE & 32)) load_u(s + 1, unxt);
           }
+          if (IDF_WINO_SCHED == 3 && i == 1 && !(IDF_WINO_ABLATE & 32)) load_u(s + 1, unxt);
+        }
+        if (IDF_WINO_SCHED == 3 && i == 3 && s + 2 < s_hi && !(IDF_WINO_ABLATE & 1)) {
+#pragma unroll
+          for (int m = 3; m < XI_PER_W; ++m) issue_piece(s + 2, buf, m);
         }
         if (i == 2 && !(IDF_WINO_ABLATE & 16)) __syncthreads();
       }
