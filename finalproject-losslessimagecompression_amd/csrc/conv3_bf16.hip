@@ -18,7 +18,9 @@
 // conflicts) and the slab's 9 x 4 x n_alloc x 16 B of weights, double-buffered: slab s+1's
 // DMA is in flight under slab s's 108 MFMAs per wave; one barrier per slab.  Within a slab
 // the 9 taps are software-pipelined (tap t+1's 4 + NF fragment reads issued before tap t's
-// MFMAs).
+// MFMAs).  The shadow's pitch is a multiple of 64 channels (dense_block_run), so a pixel's
+// 32-channel slab is one 64-B run inside one 128-B line: with an 8-channel pitch half the runs
+// straddled two lines and the L0 c=496 launch took 806 instead of 650 us.
 // The sum order (slab-major, tap-minor, 32 channels per MFMA) depends on the weights' shape
 // only; small images split the slabs (from H, W -- never the batch) with a fixed-order reduce:
 // deterministic and batch-invariant, so the decoder reproduces the encoder exactly.

@@ -553,7 +553,8 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
     if (!blk->fold) return IDF_ERR_ARG;
     for (int i = 0; i < blk->depth; ++i)
       if (!blk->wb16[i]) return IDF_ERR_ARG;
-    ld16 = ((int64_t)blk->k_in[blk->depth] + 7) / 8 * 8;
+    // pitch a multiple of 64 channels: a pixel's 32-channel slab is one aligned 64-B run
+    ld16 = ((int64_t)blk->k_in[blk->depth] + 63) / 64 * 64;
     const int64_t sh = (P * ld16 / 2 + 3) / 4 * 4;  // floats
     if (sh > ws_floats) return IDF_ERR_WORKSPACE;
     f16 = (uint16_t*)tmp;

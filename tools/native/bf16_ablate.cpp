@@ -32,7 +32,7 @@ int main() {
   const int N = 44, n_alloc = 48;
   for (auto& cs : cases) {
     const int64_t P = (int64_t)cs.B * cs.hw * cs.hw;
-    const int ld = (cs.c + N + 15) / 16 * 16, ld16 = (cs.c + N + 15) / 8 * 8;
+    const int ld = (cs.c + N + 15) / 16 * 16, ld16 = (cs.c + N + 63) / 64 * 64;
     const int nslab = (cs.c + 31) / 32;
     float* X = dev_random<float>((size_t)P * ld, false);
     uint16_t* X16 = dev_random<uint16_t>((size_t)P * ld16, true);
