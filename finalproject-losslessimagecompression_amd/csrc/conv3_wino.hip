@@ -435,6 +435,18 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
         Y[1][0] = (u1[0] + u1[1]) + u1[2];
         Y[1][1] = (u1[1] - u1[2]) - u1[3];
         const int b = b0 + img;
+        // residual loads for the 2x2 outputs before any of their stores
+        float rv[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+        if (g.res && g.ksplit == 1) {
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+              const int y = y0 + 2 * ty + r, x = x0 + 2 * tx + c;
+              if (b < g.B && y < g.H && x < g.Wd)
+                rv[r][c] = g.res[(((int64_t)b * g.H + y) * g.Wd + x) * g.ldr + n];
+            }
+        }
 #pragma unroll
         for (int r = 0; r < 2; ++r)
 #pragma unroll
@@ -444,7 +456,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
             const int64_t p = ((int64_t)b * g.H + y) * g.Wd + x;
             if (g.ksplit == 1) {
               float v = Y[r][c] + btab[bias_class(y, x, g.H, g.Wd) * (NF * 16) + n - nf0 * 16];
-              if (g.res) v = g.res[p * g.ldr + n] + v;
+              if (g.res) v = rv[r][c] + v;
               g.out[p * g.ldo + n] = wact(v, g.act, g.slope);
             }
             else

@@ -159,25 +159,35 @@ __global__ void __launch_bounds__(256) conv_taps_kernel(ConvTapsArgs g) {
     __syncthreads();
   }
 
+  // bias loads first (a load after a store to a possibly aliasing pointer would wait for it),
+  // then one pixel decomposition per output row (32-bit: the host caps P below 2^31)
+  float bv[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int n = n0 + wn * WTN + j * 16 + lr;
-    if (n >= g.N) continue;
-    const float bv = g.bias ? g.bias[n] : 0.0f;
+    bv[j] = g.bias && n < g.N ? g.bias[n] : 0.0f;
+  }
+  const uint32_t hwc32 = (uint32_t)hwc, wc32 = (uint32_t)g.Wc;
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t p = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
-        if (p >= g.P) continue;
-        const int64_t b = p / hwc, rem = p - b * hwc;
-        const int m = (int)(rem / g.Wc), nn = (int)(rem - (int64_t)m * g.Wc);
-        const int64_t o = (b * g.Ho + (int64_t)m * g.osy + g.oy0) * g.Wo + (int64_t)nn * g.osx + g.ox0;
-        float v = acc[i][j][r] + bv;
+    for (int r = 0; r < 4; ++r) {
+      const int64_t p = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+      if (p >= g.P) continue;
+      const uint32_t p32 = (uint32_t)p;
+      const uint32_t b = p32 / hwc32, rem = p32 - b * hwc32;
+      const uint32_t m = rem / wc32, nn = rem - m * wc32;
+      const int64_t o = ((int64_t)b * g.Ho + (int64_t)m * g.osy + g.oy0) * g.Wo +
+                        (int64_t)nn * g.osx + g.ox0;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * WTN + j * 16 + lr;
+        if (n >= g.N) continue;
+        float v = acc[i][j][r] + bv[j];
         if (g.res) v = g.res[o * g.ldr + n] + v;  // ResBlock: x + resblock(x) (nnblock.py:81-82)
         g.out[o * g.ldo + n] = vq_act(v, g.act, g.slope);
       }
-  }
+    }
 }
 
 template <int BN>
@@ -440,6 +450,7 @@ int idf_conv_taps_f32(void* stream, int32_t B, int32_t Hi, int32_t Wi, int32_t C
   a.Ho = Ho; a.Wo = Wo; a.osy = osy; a.osx = osx; a.oy0 = oy0; a.ox0 = ox0;
   a.res = res; a.ldr = ld_res; a.act = act; a.slope = slope;
   a.P = (int64_t)B * Hc * Wc;
+  if (a.P >= ((int64_t)1 << 31)) return IDF_ERR_UNSUPPORTED;  // 32-bit pixel decomposition
   const int bn = N <= 32 ? 32 : (N <= 64 ? 64 : 128);
   if (n_alloc < ((N + bn - 1) / bn) * bn) return IDF_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
