@@ -27,7 +27,7 @@
 //     with the next tile-fragment's LDS reads issued ahead of each MFMA group.
 // After the last slab the accumulators (M) go through LDS one n-fragment at a time for
 // the cross-position output transform, bias (incl. the folded 1x1 bias per valid tap),
-// activation and store.  Small images split the slab range (ksplit, fixed by H, W, C)
+// activation and store.  Small images split the slab range (ksplit, fixed by H, W, C, N)
 // into partial Y tiles that conv3_wino_reduce_kernel sums in fixed order.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -491,7 +491,7 @@ struct WinoPlan {
 // tiled as the next even size: the extra row/column of 2x2 tiles reads zero padding
 // (out-of-image halo) and its outputs are never stored, so every stored pixel sees the
 // same 3x3 neighbourhood as in the direct conv.
-static WinoPlan wino_plan(int H, int W, int nslab) {
+static WinoPlan wino_plan(int H, int W, int nslab, int N) {
   WinoPlan pl = {0, 1, 0, 0, 1, 0};
   if (H < 1 || W < 1) return pl;
   const int He = (H + 1) & ~1, We = (W + 1) & ~1;
@@ -519,6 +519,12 @@ static WinoPlan wino_plan(int H, int W, int nslab) {
   if (halo > kWMaxHalo) return pl;
   const int px = H * W;
   pl.ksplit = px <= 64 ? 4 : (px <= 144 ? 2 : 1);
+  // Blocks come from the pixels, the n-tiles and the split.  Packed small images (64 tiles of
+  // whole images per block) and wide outputs (several n-tiles: the VQ-VAE's 384/512-channel
+  // convs) have enough blocks without splitting K, and the split's partial-sum round trip
+  // and reduce then cost more than they gain (measured: config 4 5.4 -> 8.3 Mpx/s, config 3's
+  // VQ-VAE 67 -> 54 ms; imagenet64's 8x8 level keeps 4: 10.2 vs 9.6 Mpx/s with 1).
+  if (pl.big || N > 64) pl.ksplit = 1;
   if (pl.ksplit > nslab) pl.ksplit = nslab > 0 ? nslab : 1;
   pl.ok = 1;
   return pl;
@@ -529,12 +535,12 @@ static WinoPlan wino_plan(int H, int W, int nslab) {
 using namespace idf;
 
 extern "C" int idf_conv3x3_wino_supported(int32_t H, int32_t W) {
-  return wino_plan(H, W, 1).ok;
+  return wino_plan(H, W, 1, 1).ok;
 }
 
 extern "C" int64_t idf_conv3x3_wino_workspace(int32_t B, int32_t H, int32_t W, int32_t C,
                                               int32_t N) {
-  WinoPlan pl = wino_plan(H, W, (C + 15) / 16);
+  WinoPlan pl = wino_plan(H, W, (C + 15) / 16, N);
   if (!pl.ok || pl.ksplit <= 1) return 0;
   return (int64_t)pl.ksplit * B * H * W * ((N + 3) / 4 * 4);
 }
@@ -552,7 +558,7 @@ static int wino_launch(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
   WinoArgs g = {};
   g.X = x; g.ldx = ld_x; g.C = C; g.U = u; g.nslab = (C + 15) / 16; g.nft = nft; g.N = N;
   g.B = B; g.H = H; g.Wd = W;
-  WinoPlan pl = wino_plan(H, W, g.nslab);
+  WinoPlan pl = wino_plan(H, W, g.nslab, N);
   if (!pl.ok) return IDF_ERR_UNSUPPORTED;
   // per-block buffer offsets are 32-bit: the block's images must span < 4 GiB
   if ((int64_t)pl.IMGS * H * W * ld_x * 4 >= (int64_t)kWInvalid) return IDF_ERR_UNSUPPORTED;
