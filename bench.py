@@ -45,6 +45,32 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed PMC passes
+    (profiles/<round>/pmc_bench/{fetch,write}.csv, written by tools/pmc_bench.sh over this
+    bench): mean over its dispatches of 2 x FETCH_SIZE (the gfx950 correction for
+    16-B-per-lane streaming reads, MI355X_MICROARCH.md "HBM") + WRITE_SIZE, KiB -> bytes.
+    None when no such profile exists."""
+    import csv
+    import glob
+    fetch = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_bench", "fetch.csv")))
+    if not fetch:
+        return None, None
+    d = os.path.dirname(fetch[-1])
+
+    def mean(name):
+        path = os.path.join(d, name)
+        if not os.path.exists(path):
+            return None
+        v = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+             if kernel in r["Kernel_Name"]]
+        return sum(v) / len(v) if v else None
+    f, w = mean("fetch.csv"), mean("write.csv")
+    if f is None or w is None:
+        return None, None
+    return (2.0 * f + w) * 1024.0, os.path.relpath(d, REPO)
+
+
 def conv_kernel_name(eng):
     from idfcodec import engine
     if eng.wino:
@@ -204,6 +230,7 @@ def main():
     _lib.lib().idf_timer_destroy(timer)
 
     flops = eng.flops_per_image()["total"]
+    traffic, traffic_src = pmc_traffic("conv3_wino_kernel<3, 448>") if eng.wino else (None, None)
     step_ms = elapsed / args.steps * 1e3
     px_total = world * B * PX_PER_IMG * args.steps
     value = px_total / elapsed / 1e6
@@ -252,7 +279,9 @@ def main():
                 "peak": PEAK_F32_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(c3_tflops / PEAK_F32_TFLOPS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_unit": "B/launch (HBM, PMC)",
+                "traffic_source": traffic_src,
                 "avg_launch_ms": round(c3_avg_ms, 5),
                 "mfma_executed_tflops": round(c3_tflops * wino_exec_ratio(eng), 3),
                 "conv1x1_achieved": round(c1_tflops, 3),
