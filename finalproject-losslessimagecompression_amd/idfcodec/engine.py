@@ -228,6 +228,11 @@ class FlowEngine:
                               for l in range(self.nsplit)]
         blocks = [b for lv in self.couple for b in lv] + self.prior
         self.ld_feat = max(b.geom.ld_feat for b in blocks)
+        # tmp: split-K partials (f32); bf16 blocks also keep their bf16 feature shadow at its
+        # front (pitch round_up(k, 64) bf16 = half as many floats) ahead of 2-way partials
+        self.ld_tmp = self.ld_feat
+        if self.precision == "bf16":
+            self.ld_tmp = max(self.ld_feat, round_up(self.ld_feat, 64) // 2 + 2 * 48 + 8)
         self._ws = {}
         self._top_prior = None
 
@@ -263,7 +268,7 @@ class FlowEngine:
             "img": f(B * self.H * self.W * 4),
             "x": [[f(B * L.h * L.w * L.ldx), f(B * L.h * L.w * L.ldx)] for L in self.levels],
             "feat": f(Pmax * self.ld_feat),
-            "tmp": f(Pmax * self.ld_feat),
+            "tmp": f(Pmax * self.ld_tmp),
             "lat": f(B * self.n_sym_img),
             "mean": f(B * self.n_sym_img),
             "logscale": f(B * self.n_sym_img),
@@ -327,7 +332,7 @@ class FlowEngine:
             check(L.idf_copy_cols(s, P, 0, a_pad, None, 0, ptr(feat), ld), "zero cols")
         else:
             check(L.idf_copy_cols(s, P, nx, a_pad, x_src, ld_src, ptr(feat), ld), "copy cols")
-        blk.run(s, B, Lv.h, Lv.w, ptr(feat), ld, ptr(ws["tmp"]), ld,
+        blk.run(s, B, Lv.h, Lv.w, ptr(feat), ld, ptr(ws["tmp"]), self.ld_tmp,
                 head_prior(Lv.z, mean, logscale, scale))
 
     def _top_prior_cached(self, ws, B, s, off):
@@ -369,7 +374,7 @@ class FlowEngine:
                                               self.ld_feat), "permute")
                 self._swap(ws, l)
                 xo = ptr(x2) + Lv.a * FLOAT
-                blk.run(s, B, Lv.h, Lv.w, ptr(ws["feat"]), self.ld_feat, ptr(ws["tmp"]), self.ld_feat,
+                blk.run(s, B, Lv.h, Lv.w, ptr(ws["feat"]), self.ld_feat, ptr(ws["tmp"]), self.ld_tmp,
                         head_couple(_lib.EPI_COUPLE_ADD, xo, Lv.ldx))
             x, x2 = self._x(ws, l), self._x(ws, l, 1)
             check(L.idf_permute_couple_in(s, P, Lv.C, ptr(self.ids[l][self.nflows]), ptr(x), Lv.ldx,
@@ -438,7 +443,7 @@ class FlowEngine:
                 check(L.idf_copy_cols(s, P, Lv.a, blk.geom.a_pad, ptr(x), Lv.ldx, ptr(ws["feat"]),
                                       self.ld_feat), "copy cols")
                 xo = ptr(x) + Lv.a * FLOAT
-                blk.run(s, B, Lv.h, Lv.w, ptr(ws["feat"]), self.ld_feat, ptr(ws["tmp"]), self.ld_feat,
+                blk.run(s, B, Lv.h, Lv.w, ptr(ws["feat"]), self.ld_feat, ptr(ws["tmp"]), self.ld_tmp,
                         head_couple(_lib.EPI_COUPLE_SUB, xo, Lv.ldx))
                 check(L.idf_permute_couple_in(s, P, Lv.C, ptr(self.inv_ids[l][k]), ptr(x), Lv.ldx,
                                               ptr(x2), Lv.ldx, 0, 0, None, 0), "permute")

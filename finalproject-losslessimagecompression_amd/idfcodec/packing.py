@@ -229,6 +229,10 @@ def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
                 w64[:g][:, :, pos] = wf64
                 wus.append(wino_weights(w64, ldw3 // 16))
             if bf16:
+                if g_alloc > 48:
+                    raise NotImplementedError(
+                        f"bf16 DenseLayer convs take growth <= 48 per layer (conv3_bf16.hip: "
+                        f"one 48-output tile per block); this layer grows by {g}")
                 wbs.append(bf16_weights(w3p, k))
             vp = np.zeros((9, g_alloc), np.float32)
             vp[:, :g] = v

@@ -100,3 +100,25 @@ def test_bf16_flow_round_trip_config3():
     x = synthetic.images(2, H=size[0], W=size[1], seed=8).cuda()
     out, info = codec.decode(codec.encode(x))
     assert info["ok"] and torch.equal(out, x)
+
+
+@pytest.mark.parametrize("H,growth,depth", [(16, 24, 3), (8, 40, 2), (12, 120, 4)])
+def test_bf16_small_flow_round_trip_and_batch_invariance(H, growth, depth):
+    """Small bf16 flows (narrow DenseBlocks: the bf16 shadow + split-K partials share tmp;
+    8x8 levels take the 2-way split): exact round trip, and an image coded alone gives the
+    same streams as inside the batch."""
+    from idfcodec import synthetic
+    from idfcodec.configs import _dense, _flows
+    cfg = _flows("IDFlows", 2, 2, H, H, 3, _dense(growth, depth), _dense(growth, depth), 2)
+    model = synthetic.build_model(cfg).cuda()
+    model.idf_precision = "bf16"
+    assert model.engine().precision == "bf16"
+    x = synthetic.images(3, H=H, W=H, seed=H + growth).cuda()
+    codec = model.codec()
+    bs = codec.encode(x)
+    out, info = codec.decode(bs)
+    assert info["ok"] and torch.equal(out, x)
+    one = codec.encode(x[1:2].contiguous())
+    L = len(bs.level_shapes)
+    for l in range(L):
+        assert int(one.states[l]) == int(bs.states[l * 3 + 1])
