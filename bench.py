@@ -30,6 +30,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 PEAK_F32_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 matrix (f32-in MFMA) = vector peak
+PEAK_F16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 dense MFMA peak
 B_PER_GPU = 256
 PX_PER_IMG = 64 * 64
 
@@ -73,6 +74,11 @@ def pmc_traffic(kernel: str):
 
 def conv_kernel_name(eng):
     from idfcodec import engine
+    if eng.wino and eng.conv_mode == "x3":
+        return ("conv3_wino_kernel<3, 448, true, false> (+conv3_wino_reduce_kernel at 8x8): "
+                "DenseLayer 3x3 conv with the 1x1 folded in, Winograd F(2x2,3x3), split-f16 "
+                "products (f32 operands as f16 hi/lo pairs, 3 x v_mfma_f32_16x16x16_f16, f32 "
+                "accumulation)")
     if eng.wino:
         return ("conv3_wino_kernel<3> (+conv3_wino_reduce_kernel at 8x8): DenseLayer 3x3 conv "
                 "with the 1x1 folded in, Winograd F(2x2,3x3), f32 MFMA")
@@ -90,7 +96,8 @@ def wino_exec_ratio(eng):
     (43 real growth channels -> 48).  1.0 for the direct kernels."""
     if not eng.wino:
         return 1.0
-    return 16.0 / 36.0 * 48.0 / 43.0
+    r = 16.0 / 36.0 * 48.0 / 43.0
+    return 3.0 * r if eng.conv_mode == "x3" else r  # x3: three f16 MFMA passes per product
 
 
 def cpu_baseline(model_cfg, n_img):
@@ -230,7 +237,11 @@ def main():
     _lib.lib().idf_timer_destroy(timer)
 
     flops = eng.flops_per_image()["total"]
-    traffic, traffic_src = pmc_traffic("conv3_wino_kernel<3, 448>") if eng.wino else (None, None)
+    kname = ("conv3_wino_kernel<3, 448, true, false>" if eng.conv_mode == "x3"
+             else "conv3_wino_kernel<3, 448, false")
+    traffic, traffic_src = pmc_traffic(kname) if eng.wino else (None, None)
+    # the x3 kernel's products run on f16 MFMA: price them against the f16 dense peak
+    peak = PEAK_F16_TFLOPS if (eng.wino and eng.conv_mode == "x3") else PEAK_F32_TFLOPS
     step_ms = elapsed / args.steps * 1e3
     px_total = world * B * PX_PER_IMG * args.steps
     value = px_total / elapsed / 1e6
@@ -276,14 +287,16 @@ def main():
                                     "channels of the layer; averaged over the sampled launches)",
                 "bound": "mfma",
                 "achieved": round(c3_tflops, 3),
-                "peak": PEAK_F32_TFLOPS,
+                "peak": peak,
                 "unit": "TFLOP/s",
-                "frac": round(c3_tflops / PEAK_F32_TFLOPS, 4),
+                "frac": round(c3_tflops / peak, 4),
+                "conv_mode": eng.conv_mode,
                 "traffic": traffic,
                 "traffic_unit": "B/launch (HBM, PMC)",
                 "traffic_source": traffic_src,
                 "avg_launch_ms": round(c3_avg_ms, 5),
                 "mfma_executed_tflops": round(c3_tflops * wino_exec_ratio(eng), 3),
+                "mfma_executed_frac": round(c3_tflops * wino_exec_ratio(eng) / peak, 4),
                 "conv1x1_achieved": round(c1_tflops, 3),
                 "conv1x1_avg_launch_ms": round(c1_avg_ms, 5),
             },

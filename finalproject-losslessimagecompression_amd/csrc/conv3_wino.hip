@@ -40,7 +40,8 @@
 
 // Timing-only ablations for tools/native/wino_ablate (never set in the library build):
 // bit 0 skips the per-slab DMA, bit 1 skips the halo LDS reads, bit 2 skips the MFMAs,
-// bit 3 skips the input transform, bit 4 the in-loop barrier, bit 5 the U loads.
+// bit 3 skips the input transform, bit 4 the in-loop barrier, bit 5 the U loads, bit 6
+// makes every halo DMA piece read 1 KiB of contiguous (wrong) memory.
 #ifndef IDF_WINO_ABLATE
 #define IDF_WINO_ABLATE 0
 #endif
@@ -54,6 +55,8 @@
 namespace idf {
 
 typedef float w4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
 struct WinoArgs {
   const float* X;
@@ -77,7 +80,17 @@ struct WinoArgs {
   int32_t ldp;
   const float* res;  // optional residual added before the activation (VQ-VAE ResBlock)
   int64_t ldr;
+  // split-f16 mode (X3): U holds (hi, lo) f16 pairs of U * 2^k; yscale = 2^-k undoes it.
+  float yscale;
+  uint32_t* flag;  // X3: bit 0 set when the range guard trips
+  int32_t check_in;  // X3: also range-check every transformed input V (block inputs)
 };
+
+// X3 range guard: |V| below this keeps hi = f16(V) finite (f16 max 65504) with margin.
+// Layer outputs are checked against kX3OutGuard instead (|V| <= 4 max |input|), so that
+// only a block's first layer (its inputs come from elsewhere) checks V in the main loop.
+constexpr float kX3Guard = 32768.0f;
+constexpr float kX3OutGuard = 8192.0f;
 
 constexpr int kWThreads = 512;
 constexpr int kWMaxHalo = 400;   // halo pixel slots used per stage
@@ -116,12 +129,52 @@ template <int a> struct BT {
   static constexpr bool neg1 = a == 0 || a == 3;
 };
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
 template <bool NEG0, bool NEG1>
-__device__ __forceinline__ w4 comb(w4 x0, w4 x1) {
+__device__ __forceinline__ f2 comb2(f2 x0, f2 x1) {
   if (!NEG0 && !NEG1) return x0 + x1;
   if (!NEG0 && NEG1) return x0 - x1;
   if (NEG0 && !NEG1) return x1 - x0;
   return -(x0 + x1);
+}
+
+// s0*x0 + s1*x1 per channel, as two packed (v_pk_add_f32) halves
+template <bool NEG0, bool NEG1>
+__device__ __forceinline__ w4 comb(w4 x0, w4 x1) {
+  const f2 a = comb2<NEG0, NEG1>(__builtin_shufflevector(x0, x0, 0, 1),
+                                 __builtin_shufflevector(x1, x1, 0, 1));
+  const f2 b = comb2<NEG0, NEG1>(__builtin_shufflevector(x0, x0, 2, 3),
+                                 __builtin_shufflevector(x1, x1, 2, 3));
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3);
+}
+
+// f16 pair split of four f32 values: h = f16(v) (nearest even), l = f16(v - h) (nearest
+// even; v - h is exact in f32).  l comes from v_fma_mix{lo,hi}_f16, which reads h as f16
+// and v as f32 and rounds fma(-h, 1, v) once: one instruction per value.  The trailing
+// s_nop covers the VALU-write -> MFMA-operand-read wait states the compiler cannot see
+// through inline asm.
+#ifndef IDF_X3_ASM_SPLIT
+#define IDF_X3_ASM_SPLIT 0
+#endif
+__device__ __forceinline__ void split_f16(const w4& v, h4& h, h4& l) {
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  h = __builtin_convertvector(v, h4);
+  if (!IDF_X3_ASM_SPLIT) {
+    l = __builtin_convertvector(v - __builtin_convertvector(h, w4), h4);
+    return;
+  }
+  const h2 ha = __builtin_shufflevector(h, h, 0, 1), hb = __builtin_shufflevector(h, h, 2, 3);
+  uint32_t la, lb;
+  asm("v_fma_mixlo_f16 %0, -%2, 1.0, %4 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %1, -%3, 1.0, %6 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, -%2, 1.0, %5 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %1, -%3, 1.0, %7 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "s_nop 1"
+      : "=&v"(la), "=&v"(lb)
+      : "v"(ha), "v"(hb), "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
+  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+  l = __builtin_bit_cast(h4, u2{la, lb});
 }
 
 // Column slot of halo column j (0..3) relative to a tile's even-half base, de-interleaved.
@@ -191,18 +244,111 @@ struct WinoRole {
       }
     }
   }
+
+  // Split-f16 form: V = Vh + Vl and U' = Uh + Ul (f16 pairs, U' = U * 2^k formed in float64
+  // on the host), V.U' ~= Vl.Uh + Vh.Ul + Vh.Uh with f32 accumulation -- every product
+  // of two f16 values is exact in f32, the dropped Vl.Ul term is ~2^-22 of V.U'.  One
+  // v_mfma_f32_16x16x16_f16 takes the lane's channel quad (the same A/B lane map as the four
+  // 16x16x4 f32 k-steps above), so the three passes replace four f32 k-steps.  gmax tracks
+  // max |V| for the range guard.
+  template <typename Hook>
+  __device__ __forceinline__ static void mfma_x3(const w4& v0, const w4& v1, const w4 (&u)[2][NF],
+                                                 w4 (&acc)[NF * 2], float& gmax, bool check,
+                                                 Hook&& hook) {
+    h4 h0, l0, h1, l1;
+    split_f16(v0, h0, l0);
+    split_f16(v1, h1, l1);
+    if (check) {  // wave-uniform: only where the inputs are not already range-checked
+      gmax = fmaxf(fmaxf(gmax, fabsf(v0[0])), fabsf(v0[1]));
+      gmax = fmaxf(fmaxf(gmax, fabsf(v0[2])), fabsf(v0[3]));
+      gmax = fmaxf(fmaxf(gmax, fabsf(v1[0])), fabsf(v1[1]));
+      gmax = fmaxf(fmaxf(gmax, fabsf(v1[2])), fabsf(v1[3]));
+    }
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      if (p) hook(p - 1);
+#pragma unroll
+      for (int jn = 0; jn < NF; ++jn) {
+        const h8 ua = __builtin_bit_cast(h8, u[0][jn]), ub = __builtin_bit_cast(h8, u[1][jn]);
+        const h4 ua_h = __builtin_shufflevector(ua, ua, 0, 1, 2, 3);
+        const h4 ua_l = __builtin_shufflevector(ua, ua, 4, 5, 6, 7);
+        const h4 ub_h = __builtin_shufflevector(ub, ub, 0, 1, 2, 3);
+        const h4 ub_l = __builtin_shufflevector(ub, ub, 4, 5, 6, 7);
+        if (IDF_WINO_ABLATE & 4) {
+          acc[jn][p] += (float)(h0[p] * ua_h[p]);
+          acc[NF + jn][p] += (float)(h1[p] * ub_l[p]);
+          continue;
+        }
+        if (p == 0) {
+          acc[jn] = __builtin_amdgcn_mfma_f32_16x16x16f16(l0, ua_h, acc[jn], 0, 0, 0);
+          acc[NF + jn] = __builtin_amdgcn_mfma_f32_16x16x16f16(l1, ub_h, acc[NF + jn], 0, 0, 0);
+        } else if (p == 1) {
+          acc[jn] = __builtin_amdgcn_mfma_f32_16x16x16f16(h0, ua_l, acc[jn], 0, 0, 0);
+          acc[NF + jn] = __builtin_amdgcn_mfma_f32_16x16x16f16(h1, ub_l, acc[NF + jn], 0, 0, 0);
+        } else {
+          acc[jn] = __builtin_amdgcn_mfma_f32_16x16x16f16(h0, ua_h, acc[jn], 0, 0, 0);
+          acc[NF + jn] = __builtin_amdgcn_mfma_f32_16x16x16f16(h1, ub_h, acc[NF + jn], 0, 0, 0);
+        }
+      }
+    }
+    hook(2);
+  }
+
+  // The two halves of mfma_x3 for the software-pipelined loop: the split of a group's V
+  // (VALU) and its 18 MFMAs, so that the split of group t+1 can interleave with t's MFMAs.
+  template <bool CHECK>
+  __device__ __forceinline__ static void split_pair(const w4& v0, const w4& v1, h4 (&hl)[4],
+                                                    float& gmax, bool valid) {
+    split_f16(v0, hl[0], hl[1]);
+    split_f16(v1, hl[2], hl[3]);
+    if constexpr (CHECK) {  // valid = false for the pipeline's overrun past the last slab
+      float m = fmaxf(fmaxf(fabsf(v0[0]), fabsf(v0[1])), fabsf(v0[2]));
+      m = fmaxf(fmaxf(m, fabsf(v0[3])), fabsf(v1[0]));
+      m = fmaxf(fmaxf(m, fabsf(v1[1])), fabsf(v1[2]));
+      m = fmaxf(m, fabsf(v1[3]));
+      gmax = valid ? fmaxf(gmax, m) : gmax;
+    }
+  }
+  __device__ __forceinline__ static void mfma_hl(const h4 (&hl)[4], const w4 (&u)[2][NF],
+                                                 w4 (&acc)[NF * 2]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int jn = 0; jn < NF; ++jn) {
+        const h8 ua = __builtin_bit_cast(h8, u[0][jn]), ub = __builtin_bit_cast(h8, u[1][jn]);
+        const h4 ua_h = __builtin_shufflevector(ua, ua, 0, 1, 2, 3);
+        const h4 ua_l = __builtin_shufflevector(ua, ua, 4, 5, 6, 7);
+        const h4 ub_h = __builtin_shufflevector(ub, ub, 0, 1, 2, 3);
+        const h4 ub_l = __builtin_shufflevector(ub, ub, 4, 5, 6, 7);
+        const h4 a0 = p == 1 ? hl[0] : (p == 0 ? hl[1] : hl[0]);
+        const h4 a1 = p == 1 ? hl[2] : (p == 0 ? hl[3] : hl[2]);
+        const h4 b0 = p == 1 ? ua_l : ua_h, b1 = p == 1 ? ub_l : ub_h;
+        if (IDF_WINO_ABLATE & 4) {
+          acc[jn][p] += (float)a0[p];
+          continue;
+        }
+        acc[jn] = __builtin_amdgcn_mfma_f32_16x16x16f16(a0, b0, acc[jn], 0, 0, 0);
+        acc[NF + jn] = __builtin_amdgcn_mfma_f32_16x16x16f16(a1, b1, acc[NF + jn], 0, 0, 0);
+      }
+  }
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-template <int NF, int SLOTS>
+template <int NF, int SLOTS, bool X3, bool CHK = false>
 __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   // one stage = the slab's halo image [4 quads][SLOTS][4 floats]
   constexpr int STAGE = 4 * SLOTS * 4;
   constexpr int XI_PER_W = (4 * SLOTS / 64 + 7) / 8;  // halo DMA instructions per wave
   constexpr int MS = 16 * 64 * kWMsPitch;  // output-transform staging, aliases the stages
   constexpr int BT = 16 * NF * 16;         // epilogue bias table, after the staging
-  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE > MS + BT ? 2 * STAGE : MS + BT];
+  // X3 with the standard stage: U also goes through LDS (two [16 pos][NF][64][4] stages after
+  // the halo stages) so that the loop holds no ordinary global load -- see run_x3 below.
+  constexpr bool PIPE = X3 && SLOTS == kWSlots;
+  constexpr int USTAGE = 16 * NF * 256;
+  constexpr int DMA_SINK = 2 * STAGE + 2 * USTAGE;  // PIPE: 1 KiB target of idle DMA pieces
+  constexpr int LOOP_LDS = PIPE ? DMA_SINK + 256 : 2 * STAGE;
+  __shared__ __attribute__((aligned(16))) float lds[LOOP_LDS > MS + BT ? LOOP_LDS : MS + BT];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -246,6 +392,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
         const int y = y0 + hy - 1, x = x0 + hx - 1;
         if (b0 + img < g.B && y >= 0 && y < g.H && x >= 0 && x < g.Wd)
           x_src[m] = (uint32_t)(((((int64_t)img * g.H + y) * g.Wd + x) * g.ldx + 4 * q) * 4);
+        if (IDF_WINO_ABLATE & 64) x_src[m] = (uint32_t)((f * 64 + lane) * 16);  // coalesced, wrong
       }
     }
   }
@@ -266,6 +413,24 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   auto issue = [&](int slab, int buf) {
 #pragma unroll
     for (int m = 0; m < XI_PER_W; ++m) issue_piece(slab, buf, m);
+  };
+  // Branch-free form for the pipelined X3 loop: every wave issues exactly XI_PER_W pieces
+  // (idle ones read zeros into a sink), so a piece can be scheduled between MFMAs.
+  int pc_dst[XI_PER_W], pc_q4[XI_PER_W];
+#pragma unroll
+  for (int m = 0; m < XI_PER_W; ++m) {
+    const int f = wave + 8 * m;
+    const int q = f / nblk, k = f - q * nblk;
+    pc_dst[m] = f < nxi ? (q * SLOTS + 64 * k) * 4 : -1;
+    pc_q4[m] = 4 * q;
+  }
+  auto issue_piece_bf = [&](int slab, int buf, int m) {
+    const int c0 = slab * 16;
+    const bool live = pc_dst[m] >= 0;
+    const bool ok = live && x_src[m] != kWInvalid && c0 + pc_q4[m] < g.C;
+    const uint32_t off = ok ? x_src[m] + (uint32_t)c0 * 4u : kWInvalid;
+    float* dst = live ? lds + buf * STAGE + pc_dst[m] : lds + (PIPE ? DMA_SINK : 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_ptr_t)dst, 16, off, 0, 0, 0);
   };
   // this wave's two positions of U, NF fragments each, straight into registers
   auto load_u = [&](int slab, w4 (&u)[2][NF]) {
@@ -295,6 +460,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2 * NF; ++j) acc[i][j] = w4{0.f, 0.f, 0.f, 0.f};
+  float gmax = 0.0f;  // X3 range guard
 
   // The slab loop is instantiated per wave role (A, BP) so that each role's loop-invariant
   // LDS addresses are the only ones live in its loop.  Software pipeline per slab s
@@ -332,16 +498,21 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
         __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMAs
         if (IDF_WINO_SCHED == 2 && i == 1) {
           // halo pieces between group 1's k-steps, U loads after it
-          role.mfma(v0, v1, ucur, acc[i], [&](int t) {
+          auto hk = [&](int t) {
             if (more && !(IDF_WINO_ABLATE & 1) && t < XI_PER_W) issue_piece(s + 1, buf ^ 1, t);
-          });
+          };
+          if constexpr (X3) role.mfma_x3(v0, v1, ucur, acc[i], gmax, g.check_in, hk);
+          else role.mfma(v0, v1, ucur, acc[i], hk);
         } else if (IDF_WINO_SCHED == 3 && i == 3) {
           // two slabs ahead: stage buf is free once this slab's barrier (after g2) passed
-          role.mfma(v0, v1, ucur, acc[i], [&](int t) {
+          auto hk = [&](int t) {
             if (s + 2 < s_hi && !(IDF_WINO_ABLATE & 1) && t < XI_PER_W) issue_piece(s + 2, buf, t);
-          });
+          };
+          if constexpr (X3) role.mfma_x3(v0, v1, ucur, acc[i], gmax, g.check_in, hk);
+          else role.mfma(v0, v1, ucur, acc[i], hk);
         } else {
-          role.mfma(v0, v1, ucur, acc[i], [](int) {});
+          if constexpr (X3) role.mfma_x3(v0, v1, ucur, acc[i], gmax, g.check_in, [](int) {});
+          else role.mfma(v0, v1, ucur, acc[i], [](int) {});
         }
         __builtin_amdgcn_sched_barrier(0);
         if (more) {
@@ -375,20 +546,190 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
       }
     }
   };
+  // X3 pipeline.  The f16 MFMAs make a slab ~2.7x shorter than in the f32 loop, so loads get
+  // one whole slab (4 groups) to land: after slab s's barrier (which follows group g2) both
+  // the halo and the U fragments of slab s+2 are DMA'd into stage s%2 (free: its halo reads
+  // were retired before the barrier, its U is in registers), and the next barrier waits for
+  // them with vmcnt(0).  U moves by LDS-DMA as well because hipcc drains every in-flight
+  // LDS-DMA (vmcnt(0)) at the first use of an ordinary global load's result; the loop thus
+  // holds no ordinary global load, and the barriers are raw s_barriers after explicit waits
+  // (a __syncthreads() would add its own vmcnt(0) drain in the wrong place).
+  const __amdgpu_buffer_rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.U, 0, (int)((int64_t)16 * g.nslab * g.nft * 1024 < (int64_t)kWInvalid
+                               ? (int64_t)16 * g.nslab * g.nft * 1024 : (int64_t)kWInvalid),
+      0x00020000);
+  auto issue_u = [&](int slab, int buf) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int pos = 2 * wave + q;
+#pragma unroll
+      for (int j = 0; j < NF; ++j) {
+        const uint32_t off =
+            (uint32_t)((((int64_t)pos * g.nslab + slab) * g.nft + nf0 + j) * 1024 + lane * 16);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            ur, (lds_ptr_t)(lds + 2 * STAGE + buf * USTAGE + (pos * NF + j) * 256), 16, off, 0, 0, 0);
+      }
+    }
+  };
+  auto issue_u_piece = [&](int slab, int buf, int q, int j) {
+    const int pos = 2 * wave + q;
+    const uint32_t off =
+        (uint32_t)((((int64_t)pos * g.nslab + slab) * g.nft + nf0 + j) * 1024 + lane * 16);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        ur, (lds_ptr_t)(lds + 2 * STAGE + buf * USTAGE + (pos * NF + j) * 256), 16, off, 0, 0, 0);
+  };
+  auto read_u = [&](int buf, w4 (&u)[2][NF]) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int j = 0; j < NF; ++j)
+        u[q][j] = *(const w4*)(lds + 2 * STAGE + buf * USTAGE + ((2 * wave + q) * NF + j) * 256 +
+                               lane * 4);
+  };
+#ifndef IDF_WINO_STAMPS
+#define IDF_WINO_STAMPS 0
+#endif
+  // timing-only instrumentation (tools/native/wino_ablate): cycles per wave in the barrier
+  // waits, in the DMA issue after them, and in the whole loop -> g.part[block][wave][3]
+  uint64_t st_wait = 0, st_issue = 0, st_t0 = 0;
+  auto wait_barrier = [&]() {
+    uint64_t t0 = IDF_WINO_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (IDF_WINO_STAMPS) st_wait += __builtin_amdgcn_s_memtime() - t0;
+  };
+  auto run_x3 = [&](auto a_tag, auto bp_tag) {
+    constexpr int A = decltype(a_tag)::value, BP = decltype(bp_tag)::value;
+    const WinoRole<NF, A, BP> role(HWp, EH);
+    // Software pipeline over groups t = (slab s, group i): step t issues group t's 18 MFMAs
+    // interleaved with the transform + f16 split of group t+1 and the halo reads of group
+    // t+2, so each wave presents a mixed MFMA/VALU/LDS stream (two waves of a SIMD running
+    // separate VALU and MFMA phases in lockstep would serialize on the issue port).  The
+    // slab barrier sits at the start of step 2: group 3's reads were issued in step 1, and
+    // step 2 starts reading slab s+1 (its g0), whose DMA was issued after the previous
+    // barrier.
+    w4 ucur[2][NF], unxt[2][NF];
+    w4 d[2][6];
+    h4 hl[2][4];
+    if (s_lo >= s_hi) return;
+    if (IDF_WINO_STAMPS) st_t0 = __builtin_amdgcn_s_memtime();
+    if (!(IDF_WINO_ABLATE & 1)) issue(s_lo, 0);
+    if (!(IDF_WINO_ABLATE & 32)) issue_u(s_lo, 0);
+    wait_barrier();
+    role.fetch(lds + lq * SLOTS * 4, tbase[0], d[0]);
+    role.fetch(lds + lq * SLOTS * 4, tbase[1], d[1]);
+    read_u(0, ucur);
+    if (s_lo + 1 < s_hi) {
+      if (!(IDF_WINO_ABLATE & 1)) issue(s_lo + 1, 1);
+      if (!(IDF_WINO_ABLATE & 32)) issue_u(s_lo + 1, 1);
+    }
+    {
+      w4 v0, v1;
+      role.transform(d[0], v0, v1);
+      role.template split_pair<CHK>(v0, v1, hl[0], gmax, true);
+    }
+    for (int s = s_lo; s < s_hi; ++s) {
+      const int buf = (s - s_lo) & 1;
+      const bool more = s + 1 < s_hi;
+      const float* xq = lds + buf * STAGE + lq * SLOTS * 4;
+      const float* xn = lds + (buf ^ 1) * STAGE + lq * SLOTS * 4;
+      auto step = [&](auto itag) {
+        constexpr int i = decltype(itag)::value;
+        if constexpr (i == 2) {
+          if (!(IDF_WINO_ABLATE & 16)) wait_barrier();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // slab s+2's DMA into stage buf (free since this slab's barrier), spread over steps
+        // 2 (halo pieces) and 3 (U fragments) between the MFMAs; past the last slab the
+        // pieces read zeros (halo) or unused in-range bytes (U)
+        if constexpr (i == 2 && !(IDF_WINO_ABLATE & 1)) {
+#pragma unroll
+          for (int m = 0; m < XI_PER_W; ++m) issue_piece_bf(s + 2, buf, m);
+        }
+        if constexpr (i == 3 && !(IDF_WINO_ABLATE & 32)) {
+#pragma unroll
+          for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int j = 0; j < NF; ++j) issue_u_piece(s + 2, buf, q, j);
+        }
+        // branch-free step (one scheduling region): past the last slab the transform and
+        // reads run on stale, in-bounds LDS and their results are never used
+        {
+          w4 v0, v1;
+          role.transform(d[(i + 1) & 1], v0, v1);
+          role.template split_pair<CHK>(v0, v1, hl[(i + 1) & 1], gmax, i < 3 || more);
+        }
+        if constexpr (i < 2) role.fetch(xq, tbase[i + 2], d[i & 1]);
+        else role.fetch(xn, tbase[i - 2], d[i & 1]);
+        if constexpr (i == 3) read_u(buf ^ 1, unxt);
+        role.mfma_hl(hl[i & 1], ucur, acc[i]);
+        // interleave per MFMA: LDS reads first (6, or 12 with U's), DMA pieces after them
+        {
+          constexpr int ND = 6;
+          constexpr int nvm = i == 2 ? XI_PER_W : (i == 3 ? 2 * NF : 0);
+#pragma unroll
+          for (int k = 0; k < 6 * NF; ++k) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            if (k < ND) {
+              if constexpr (i == 3) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+              else __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+            } else {
+              if (k < ND + nvm) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      step(std::integral_constant<int, 0>{});
+      step(std::integral_constant<int, 1>{});
+      step(std::integral_constant<int, 2>{});
+      step(std::integral_constant<int, 3>{});
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) ucur[q][j] = unxt[q][j];
+    }
+    wait_barrier();  // the overrun DMA pieces land before the epilogue reuses the LDS
+    if (IDF_WINO_STAMPS && lane == 0 && g.part) {
+      float* o = g.part + ((int64_t)blockIdx.x * 8 + wave) * 4;
+      o[0] = (float)st_wait; o[1] = (float)st_issue;
+      o[2] = (float)(__builtin_amdgcn_s_memtime() - st_t0);
+    }
+  };
+  auto go = [&](auto a_tag, auto bp_tag) {
+    if constexpr (PIPE) run_x3(a_tag, bp_tag);
+    else run(a_tag, bp_tag);
+  };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
   using I3 = std::integral_constant<int, 3>;
   switch (wave) {
-    case 0: run(I0{}, I0{}); break;
-    case 1: run(I0{}, I1{}); break;
-    case 2: run(I1{}, I0{}); break;
-    case 3: run(I1{}, I1{}); break;
-    case 4: run(I2{}, I0{}); break;
-    case 5: run(I2{}, I1{}); break;
-    case 6: run(I3{}, I0{}); break;
-    default: run(I3{}, I1{}); break;
+    case 0: go(I0{}, I0{}); break;
+    case 1: go(I0{}, I1{}); break;
+    case 2: go(I1{}, I0{}); break;
+    case 3: go(I1{}, I1{}); break;
+    case 4: go(I2{}, I0{}); break;
+    case 5: go(I2{}, I1{}); break;
+    case 6: go(I3{}, I0{}); break;
+    default: go(I3{}, I1{}); break;
   }
+
+  if constexpr (X3) {
+    // gmax (v_max ignores NaN operands) catches out-of-range V; a NaN anywhere in V reaches
+    // the accumulators, so their sum catches it (an inf there -- only from out-of-range
+    // data or an overflowing sum -- flags too, which merely costs the fp32 recomputation)
+    float asum = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2 * NF; ++j) asum += (acc[i][j][0] + acc[i][j][1]) + (acc[i][j][2] + acc[i][j][3]);
+    if (g.check_in && (!(gmax < kX3Guard) || !(asum - asum == 0.0f)) && g.flag)
+      atomicOr(g.flag, 1u);
+  }
+
+  bool out_ok = true;  // X3: every stored output within kX3OutGuard (false on NaN)
 
   // ---- output transform, one n-fragment at a time through LDS
   float* Ms = lds;  // [16 pos][64 tiles][kWMsPitch]
@@ -434,6 +775,12 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
         Y[0][1] = (u0[1] - u0[2]) - u0[3];
         Y[1][0] = (u1[0] + u1[1]) + u1[2];
         Y[1][1] = (u1[1] - u1[2]) - u1[3];
+        if constexpr (X3) {
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) Y[r][c] = Y[r][c] * g.yscale;
+        }
         const int b = b0 + img;
         // residual loads for the 2x2 outputs before any of their stores
         float rv[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
@@ -457,7 +804,9 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
             if (g.ksplit == 1) {
               float v = Y[r][c] + btab[bias_class(y, x, g.H, g.Wd) * (NF * 16) + n - nf0 * 16];
               if (g.res) v = rv[r][c] + v;
-              g.out[p * g.ldo + n] = wact(v, g.act, g.slope);
+              v = wact(v, g.act, g.slope);
+              if constexpr (X3) out_ok = out_ok && fabsf(v) < kX3OutGuard;
+              g.out[p * g.ldo + n] = v;
             }
             else
               g.part[((int64_t)ks * ((int64_t)g.B * g.H * g.Wd) + p) * g.ldp + n] = Y[r][c];
@@ -465,6 +814,9 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
       }
     }
     __syncthreads();
+  }
+  if constexpr (X3) {
+    if (!out_ok && g.flag) atomicOr(g.flag, 1u);
   }
 }
 
@@ -480,7 +832,9 @@ __global__ void __launch_bounds__(256) conv3_wino_reduce_kernel(WinoArgs g) {
   const int y = (int)(rem / g.Wd), x = (int)(rem % g.Wd);
   float v = s + wbias(g, n, y, x);
   if (g.res) v = g.res[p * g.ldr + n] + v;
-  g.out[p * g.ldo + n] = wact(v, g.act, g.slope);
+  v = wact(v, g.act, g.slope);
+  if (g.flag && !(fabsf(v) < kX3OutGuard)) atomicOr(g.flag, 1u);  // X3 output guard
+  g.out[p * g.ldo + n] = v;
 }
 
 struct WinoPlan {
@@ -549,7 +903,8 @@ static int wino_launch(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
                        int64_t ld_x, const float* u, int32_t nft, const float* b3,
                        const float* vtap, int32_t ldv, const float* bfull, int32_t N, float* out,
                        int64_t ld_out, const float* res, int64_t ld_res, int32_t act, float slope,
-                       float* workspace, int64_t workspace_floats) {
+                       float* workspace, int64_t workspace_floats, bool x3 = false,
+                       float yscale = 1.0f, uint32_t* flag = nullptr, int check_in = 1) {
   if (B <= 0 || H <= 0 || W <= 0 || N <= 0) return IDF_OK;
   if (C <= 0 || (C & 3) || (ld_x & 3) || !u) return IDF_ERR_ARG;
   const int nf_total = (N + 15) / 16;
@@ -571,8 +926,10 @@ static int wino_launch(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
   g.b3 = b3; g.vtap = vtap; g.bfull = bfull; g.ldv = ldv; g.act = act; g.slope = slope;
   g.out = out; g.ldo = ld_out;
   g.res = res; g.ldr = ld_res;
+  g.yscale = yscale; g.flag = x3 ? flag : nullptr; g.check_in = check_in;
   if (vtap && (!bfull || ldv < N)) return IDF_ERR_ARG;
   if (res && ld_res < N) return IDF_ERR_ARG;
+  if (IDF_WINO_STAMPS) g.part = workspace;
   if (pl.ksplit > 1) {
     g.ldp = (N + 3) / 4 * 4;
     if (!workspace || workspace_floats < (int64_t)pl.ksplit * B * H * W * g.ldp)
@@ -581,21 +938,25 @@ static int wino_launch(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
   }
   const int64_t blocks = (int64_t)g.tiles_b * g.tiles_y * g.tiles_x * g.n_tiles * pl.ksplit;
   hipStream_t s = (hipStream_t)stream;
-#define IDF_WINO_LAUNCH(nf, slots) \
-  hipLaunchKernelGGL((conv3_wino_kernel<nf, slots>), dim3((unsigned)blocks), dim3(kWThreads), 0, s, g)
-  if (pl.big) {
-    switch (NF) {
-      case 1: IDF_WINO_LAUNCH(1, kWSlotsBig); break;
-      case 2: IDF_WINO_LAUNCH(2, kWSlotsBig); break;
-      default: IDF_WINO_LAUNCH(3, kWSlotsBig); break;
-    }
-  } else {
-    switch (NF) {
-      case 1: IDF_WINO_LAUNCH(1, kWSlots); break;
-      case 2: IDF_WINO_LAUNCH(2, kWSlots); break;
-      default: IDF_WINO_LAUNCH(3, kWSlots); break;
-    }
+#define IDF_WINO_LAUNCH(nf, slots, x3, chk)                                                     \
+  hipLaunchKernelGGL((conv3_wino_kernel<nf, slots, x3, chk>), dim3((unsigned)blocks),              \
+                     dim3(kWThreads), 0, s, g)
+#define IDF_WINO_NF(slots, x3, chk)                   \
+  switch (NF) {                                       \
+    case 1: IDF_WINO_LAUNCH(1, slots, x3, chk); break; \
+    case 2: IDF_WINO_LAUNCH(2, slots, x3, chk); break; \
+    default: IDF_WINO_LAUNCH(3, slots, x3, chk); break; \
   }
+  if (pl.big) {
+    if (x3) IDF_WINO_NF(kWSlotsBig, true, false) else IDF_WINO_NF(kWSlotsBig, false, false)
+  } else if (!x3) {
+    IDF_WINO_NF(kWSlots, false, false)
+  } else if (check_in) {
+    IDF_WINO_NF(kWSlots, true, true)
+  } else {
+    IDF_WINO_NF(kWSlots, true, false)
+  }
+#undef IDF_WINO_NF
 #undef IDF_WINO_LAUNCH
   if (pl.ksplit > 1) {
     const int64_t n = (int64_t)B * H * W * N;
@@ -622,4 +983,26 @@ extern "C" int idf_conv3x3_wino_res(void* stream, int32_t B, int32_t H, int32_t 
                                     float* workspace, int64_t workspace_floats) {
   return wino_launch(stream, B, H, W, C, x, ld_x, u, nft, bias, nullptr, 0, nullptr, N, out,
                      ld_out, res, ld_res, act, slope, workspace, workspace_floats);
+}
+
+extern "C" int idf_conv3x3_wx3(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
+                               const float* x, int64_t ld_x, const uint16_t* u, int32_t nft,
+                               float yscale, const float* b3, const float* vtap, int32_t ldv,
+                               const float* bfull, int32_t N, float* out, int64_t ld_out,
+                               int32_t act, float slope, uint32_t* d_flag, int32_t check_input,
+                               float* workspace, int64_t workspace_floats) {
+  return wino_launch(stream, B, H, W, C, x, ld_x, (const float*)u, nft, b3, vtap, ldv, bfull, N,
+                     out, ld_out, nullptr, 0, act, slope, workspace, workspace_floats, true,
+                     yscale, d_flag, check_input);
+}
+
+extern "C" int idf_conv3x3_wx3_res(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
+                                   const float* x, int64_t ld_x, const uint16_t* u, int32_t nft,
+                                   float yscale, const float* bias, int32_t N, float* out,
+                                   int64_t ld_out, const float* res, int64_t ld_res, int32_t act,
+                                   float slope, uint32_t* d_flag, int32_t check_input,
+                                   float* workspace, int64_t workspace_floats) {
+  return wino_launch(stream, B, H, W, C, x, ld_x, (const float*)u, nft, bias, nullptr, 0, nullptr,
+                     N, out, ld_out, res, ld_res, act, slope, workspace, workspace_floats, true,
+                     yscale, d_flag, check_input);
 }

@@ -53,6 +53,7 @@ class IdfDenseBlock(ctypes.Structure):
         ("fold", i32), ("ldv", i32), ("vtap", P * MAX_DEPTH), ("bfull", P * MAX_DEPTH),
         ("halo", i32), ("wino", i32), ("wino_nft", i32), ("wino_u", P * MAX_DEPTH),
         ("bf16", i32), ("wb16", P * MAX_DEPTH),
+        ("wx3", i32), ("wx3_yscale", f32 * MAX_DEPTH), ("wx3_u", P * MAX_DEPTH), ("range_flag", P),
     ]
 
 
@@ -99,6 +100,10 @@ SIGNATURES = {
                                         i64, i32, f32, P, i64]),
     "idf_conv3x3_wino_res": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, P, i32, P, i64,
                                             P, i64, i32, f32, P, i64]),
+    "idf_conv3x3_wx3": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, f32, P, P, i32, P,
+                                       i32, P, i64, i32, f32, P, i32, P, i64]),
+    "idf_conv3x3_wx3_res": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, f32, P, i32, P,
+                                           i64, P, i64, i32, f32, P, i32, P, i64]),
     "idf_conv3x3_bf16_workspace": (i64, [i32, i32, i32, i32, i32]),
     "idf_conv3x3_bf16": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, P, P, i32, P, i32,
                                         P, i64, P, i64, i32, i32, f32, P, i64]),

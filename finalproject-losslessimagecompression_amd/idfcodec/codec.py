@@ -25,6 +25,7 @@ from ._lib import check, lib, ptr
 RANS_L = 1 << 32
 MAGIC = b"IDFB"
 VERSION = 1
+FLAG_CONV_X3 = 1
 
 
 @dataclass
@@ -66,7 +67,10 @@ class Bitstream:
 
     # ---- container (the reference has no file format)
     def to_bytes(self) -> bytes:
-        hdr = struct.pack("<4sHHIII", MAGIC, VERSION, 0, self.n_images, len(self.level_shapes),
+        # flags bit 0: the flow's Winograd convs ran as split-f16 products (meta conv 'x3');
+        # 0: exact-f32 (every stream written before the flag existed)
+        flags = FLAG_CONV_X3 if self.meta.get("conv", "f32") == "x3" else 0
+        hdr = struct.pack("<4sHHIII", MAGIC, VERSION, flags, self.n_images, len(self.level_shapes),
                           self.n_streams)
         shapes = b"".join(struct.pack("<III", *s) for s in self.level_shapes)
         meta = struct.pack("<Q", self.n_subpixels())
@@ -77,7 +81,7 @@ class Bitstream:
 
     @classmethod
     def from_bytes(cls, buf: bytes, device=None) -> "Bitstream":
-        magic, ver, _flags, n_img, n_lvl, n_str = struct.unpack_from("<4sHHIII", buf, 0)
+        magic, ver, flags, n_img, n_lvl, n_str = struct.unpack_from("<4sHHIII", buf, 0)
         if magic != MAGIC or ver != VERSION:
             raise ValueError("not an IDF bitstream")
         o = struct.calcsize("<4sHHIII")
@@ -92,7 +96,8 @@ class Bitstream:
         w = np.frombuffer(buf, "<i4", int(nw.sum()), o).copy()
         t = lambda a: torch.from_numpy(a).to(device) if device else torch.from_numpy(a)  # noqa: E731
         return cls(n_img, [tuple(s) for s in shapes], t(st), t(nw), t(w),
-                   meta={"n_subpixels": int(nsub)})
+                   meta={"n_subpixels": int(nsub),
+                         "conv": "x3" if flags & FLAG_CONV_X3 else "f32"})
 
 
 class StreamCoder:
@@ -190,9 +195,31 @@ class ImageCodec:
         if img_u8.dtype != torch.uint8:
             raise TypeError("ImageCodec.encode expects uint8 images")
         B = img_u8.shape[0]
-        ws = self.engine.load_u8(img_u8.contiguous())
-        self.engine.forward_pm(B, cond=cond)
-        return self.coder.encode(ws, B, compact=compact)
+        return self._encode_guarded(lambda: self.engine.load_u8(img_u8.contiguous()), B, cond,
+                                    compact)
+
+    def _encode_guarded(self, load, B, cond, compact):
+        """Encode in the engine's conv mode; if the split-f16 range guard tripped (a value
+        beyond its f16 range), recompute the batch with the exact-f32 convs.  The mode that
+        produced the streams is recorded in the bitstream (meta['conv'], container flag)."""
+        eng = self.engine
+        mode = eng.conv_mode
+        if mode == "x3":
+            eng.clear_range_flag()
+        ws = load()
+        eng.forward_pm(B, cond=cond)
+        bs = self.coder.encode(ws, B, compact=compact)
+        if mode == "x3" and eng.range_flag_tripped():
+            eng.set_conv_mode("f32")
+            try:
+                ws = load()
+                eng.forward_pm(B, cond=cond)
+                bs = self.coder.encode(ws, B, compact=compact)
+            finally:
+                eng.set_conv_mode("x3")
+            mode = "f32"
+        bs.meta["conv"] = mode
+        return bs
 
     @torch.no_grad()
     def encode_nchw(self, x: torch.Tensor, cond=None, compact: bool = True) -> Bitstream:
@@ -200,9 +227,8 @@ class ImageCodec:
         configs, trainer.py:608) -> Bitstream."""
         _lib.require_device(x, "flow input")
         B = x.shape[0]
-        ws = self.engine.load_nchw(x.float().contiguous())
-        self.engine.forward_pm(B, cond=cond)
-        return self.coder.encode(ws, B, compact=compact)
+        xf = x.float().contiguous()
+        return self._encode_guarded(lambda: self.engine.load_nchw(xf), B, cond, compact)
 
     @torch.no_grad()
     def decode_nchw(self, bs: Bitstream, cond=None, verify: bool = True):
@@ -232,7 +258,15 @@ class ImageCodec:
         def dec(l, ws):
             self.coder.decode_level(bs, B, l, ws, word_off, out_state, out_status)
 
-        ws = eng.inverse_pm(B, dec, cond=cond)
+        # the convs must run as the encoder ran them (bit-identical couplings)
+        mode, prev = bs.meta.get("conv", "f32"), eng.conv_mode
+        if mode != prev:
+            eng.set_conv_mode(mode)
+        try:
+            ws = eng.inverse_pm(B, dec, cond=cond)
+        finally:
+            if mode != prev:
+                eng.set_conv_mode(prev)
         return ws, {"final_states": out_state, "status": out_status}
 
     @torch.no_grad()

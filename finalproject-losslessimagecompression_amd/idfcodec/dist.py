@@ -113,6 +113,10 @@ def merge_residual(parts):
     from .codec import Bitstream
     from .residual import ResidualBitstream
     fl = [p.flow for p in parts]
+    modes = {f.meta.get("conv", "f32") for f in fl}
+    if len(modes) != 1:
+        raise ValueError(f"shards coded with different conv modes {sorted(modes)}: re-encode "
+                         "them in one mode (ImageCodec engine.set_conv_mode) before merging")
     st = torch.cat([f.states for f in fl])
     nw = torch.cat([f.nwords.to(torch.int64) for f in fl])
     w = torch.cat([f.words for f in fl])
@@ -124,7 +128,7 @@ def _assemble(first, world, st, nw, w, idx):
     from .residual import ResidualBitstream
     fl = first.flow
     st, nw, w = interleave_levels(st, nw, w, world, len(fl.level_shapes), fl.n_images)
-    meta = {k: v for k, v in fl.meta.items() if k == "n_subpixels"}
+    meta = {k: v for k, v in fl.meta.items() if k in ("n_subpixels", "conv")}
     if "n_subpixels" in meta:
         meta["n_subpixels"] = meta["n_subpixels"] * world
     flow = Bitstream(fl.n_images * world, fl.level_shapes, st, nw, w, None, meta)
@@ -139,6 +143,16 @@ def gather_residual(rbs, dst: int = 0, group=None):
     Equal shards required.  Returns the merged bitstream on `dst`, None elsewhere."""
     world = dist.get_world_size(group)
     fl = rbs.flow
+    # every shard must have run the same conv mode (a tripped split-f16 range guard on one
+    # rank re-encodes that shard with exact-f32 convs): agree on it first
+    mode = torch.tensor([1 if fl.meta.get("conv", "f32") == "x3" else 0], dtype=torch.int64,
+                        device=fl.words.device)
+    lo, hi = mode.clone(), mode.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    if int(lo.item()) != int(hi.item()):
+        raise ValueError("shards coded with different conv modes: re-encode the x3 shards "
+                         "with engine.set_conv_mode('f32') and gather again")
     got = gather_streams(fl.states, fl.nwords, fl.words, dst=dst, group=group)
     idx = gather_padded(rbs.idx_words, dst=dst, group=group)
     if got is None:

@@ -37,6 +37,10 @@ HALO = os.environ.get("IDF_HALO", "1") != "0"
 # Folded 3x3 convs on even-sized images run as Winograd F(2x2,3x3) (conv3_wino.hip, 2.25x
 # fewer multiplies); IDF_WINO=0 keeps them on the direct halo kernel.
 WINO = os.environ.get("IDF_WINO", "1") != "0"
+# fp32 Winograd convs use split-f16 products (idf_conv3x3_wx3: each f32 operand as an f16
+# hi/lo pair, three f16 MFMAs, f32 accumulation -- fp32-class error) with a
+# range guard that falls back to the exact-f32 kernel; IDF_WX3=0 always uses the latter.
+WX3 = os.environ.get("IDF_WX3", "1") != "0"
 
 
 class DeviceBlock:
@@ -56,6 +60,7 @@ class DeviceBlock:
         self.bfull = [dev(a) for a in packed.bfull]
         self.wino_u = [dev(a) for a in packed.wino_u]
         self.wb16 = [dev(a.view(np.int16)) for a in packed.wb16]
+        self.wx3_u = [dev(a.view(np.int16)) for a in packed.wx3_u]
         d = IdfDenseBlock()
         g = self.geom
         d.depth = g.depth
@@ -90,6 +95,10 @@ class DeviceBlock:
         d.wino_nft = packed.g_alloc // 16
         for i, u in enumerate(self.wino_u):
             d.wino_u[i] = u.data_ptr()
+        d.wx3 = 1 if (d.wino and self.wx3_u) else 0
+        for i, u in enumerate(self.wx3_u):
+            d.wx3_u[i] = u.data_ptr()
+            d.wx3_yscale[i] = packed.wx3_yscale[i]
         d.bf16 = 1 if (packed.fold and self.wb16) else 0
         for i, u in enumerate(self.wb16):
             d.wb16[i] = u.data_ptr()
@@ -165,6 +174,9 @@ class FlowEngine:
         self.wino = self.fold and WINO and self.precision == "f32" and any(
             lib().idf_conv3x3_wino_supported(model.H // s, model.W // s)
             for s in [model.blocks[0]["extend"].scale ** (l + 1) for l in range(model.nsplit)])
+        self.wx3 = self.wino and WX3
+        # device word the wx3 range guard ORs into (see IdfDenseBlock.range_flag)
+        self.range_flag = torch.zeros(1, dtype=torch.int32, device=self.device)
         sd = {k: v for k, v in model.state_dict().items()}
         self.conditional = type(model).__name__ == "ConditionalFlows"
         self.conv_for_cond = bool(getattr(model, "conv_for_cond", False))
@@ -202,11 +214,12 @@ class FlowEngine:
         for l in range(self.nsplit):
             self.couple.append([DeviceBlock(pack_dense_block(
                 sd, f"blocks.{l}.flows.{2 * k + 1}.dense.", c_depth, c_act, fold=self.fold,
-                wino=self.wino, bf16=self.precision == "bf16"),
+                wino=self.wino, bf16=self.precision == "bf16", wx3=self.wx3),
                 self.device) for k in range(self.nflows)])
             self.prior.append(DeviceBlock(pack_dense_block(sd, f"blocks.{l}.prior.NN.", p_depth,
                                                            p_act, fold=self.fold, wino=self.wino,
-                                                           bf16=self.precision == "bf16"),
+                                                           bf16=self.precision == "bf16",
+                                                           wx3=self.wx3),
                                           self.device))
             ids_l, inv_l = [], []
             for k in range(self.nflows + 1):
@@ -227,6 +240,10 @@ class FlowEngine:
                                                 stride=2, padding=1), self.device)
                               for l in range(self.nsplit)]
         blocks = [b for lv in self.couple for b in lv] + self.prior
+        self._blocks = blocks
+        for b in blocks:
+            b.desc.range_flag = self.range_flag.data_ptr()
+        self.conv_mode = "x3" if self.wx3 else "f32"
         self.ld_feat = max(b.geom.ld_feat for b in blocks)
         # tmp: split-K partials (f32); bf16 blocks also keep their bf16 feature shadow at its
         # front (pitch round_up(k, 64) bf16 = half as many floats) ahead of 2-way partials
@@ -235,6 +252,26 @@ class FlowEngine:
             self.ld_tmp = max(self.ld_feat, round_up(self.ld_feat, 64) // 2 + 2 * 48 + 8)
         self._ws = {}
         self._top_prior = None
+
+    # ------------------------------------------------------------ conv mode
+    def set_conv_mode(self, mode: str):
+        """'x3' (split-f16 Winograd, needs wx3 weights) or 'f32' (exact-f32 Winograd).  The
+        decoder must run the mode the encoder ran (Bitstream.meta['conv'])."""
+        if mode not in ("x3", "f32"):
+            raise ValueError(f"conv mode must be 'x3' or 'f32', not {mode!r}")
+        if mode == "x3" and not self.wx3:
+            raise ValueError("this engine has no split-f16 (wx3) weights")
+        on = 1 if mode == "x3" else 0
+        for b in self._blocks:
+            b.desc.wx3 = on if b.wx3_u else 0
+        self.conv_mode = mode
+        self._top_prior = None  # computed under the previous mode
+
+    def clear_range_flag(self):
+        self.range_flag.zero_()
+
+    def range_flag_tripped(self) -> bool:
+        return bool(self.range_flag.item())
 
     # ------------------------------------------------------------ geometry
     def sym_offsets(self, B: int) -> list[int]:

@@ -112,6 +112,8 @@ class PackedBlock:
     ldwh: int
     wino_u: list = field(default_factory=list)  # fold+wino: wino_weights() per layer
     wb16: list = field(default_factory=list)    # fold+bf16: bf16_weights() per layer (uint16)
+    wx3_u: list = field(default_factory=list)   # fold+wino+wx3: wino_weights_x3() per layer
+    wx3_yscale: list = field(default_factory=list)
 
 
 def fold_layer(w1, b1, w3):
@@ -137,22 +139,55 @@ def fold_layer64(w1, b1, w3):
 WINO_G = np.array([[1.0, 0.0, 0.0], [0.5, 0.5, 0.5], [0.5, -0.5, 0.5], [0.0, 0.0, 1.0]])
 
 
-def wino_weights(w: np.ndarray, nslab: int) -> np.ndarray:
-    """w: [n_alloc, 9, ldw] (float64 preferred) 3x3 weights in the padded channel
-    coordinates.  Returns U = G g G^T for every (n, c), rounded once to fp32 and laid out
-    in MFMA fragment order [16 positions][nslab][nft][64 lanes][4] (lane = 16*h + r holds
-    U[pos][16*f + r][16*slab + 4*h .. +3]) -- what conv3_wino.hip streams per wave."""
+def wino_transform64(w: np.ndarray, nslab: int) -> np.ndarray:
+    """U = G g G^T in float64 for every (n, c): [16 positions][n_alloc][nslab*16], from
+    w: [n_alloc, 9, ldw] 3x3 weights in the padded channel coordinates."""
     n_alloc = w.shape[0]
     assert n_alloc % 16 == 0
-    nft = n_alloc // 16
     C = nslab * 16
     g = np.zeros((n_alloc, C, 3, 3), np.float64)
     cw = min(C, w.shape[2])
     g[:, :cw] = w[:, :, :cw].astype(np.float64).transpose(0, 2, 1).reshape(n_alloc, cw, 3, 3)
-    U = np.einsum("ai,ncij,bj->abnc", WINO_G, g, WINO_G).reshape(16, n_alloc, C)
+    return np.einsum("ai,ncij,bj->abnc", WINO_G, g, WINO_G).reshape(16, n_alloc, C)
+
+
+def wino_weights(w: np.ndarray, nslab: int, U: np.ndarray | None = None) -> np.ndarray:
+    """w: [n_alloc, 9, ldw] (float64 preferred) 3x3 weights in the padded channel
+    coordinates.  Returns U = G g G^T for every (n, c), rounded once to fp32 and laid out
+    in MFMA fragment order [16 positions][nslab][nft][64 lanes][4] (lane = 16*h + r holds
+    U[pos][16*f + r][16*slab + 4*h .. +3]) -- what conv3_wino.hip streams per wave."""
+    if U is None:
+        U = wino_transform64(w, nslab)
+    n_alloc = U.shape[1]
+    nft = n_alloc // 16
     U = U.reshape(16, nft, 16, nslab, 4, 4)          # pos, f, r, slab, h, e
     U = U.transpose(0, 3, 1, 4, 2, 5)                 # pos, slab, f, h, r, e
     return np.ascontiguousarray(U.reshape(16, nslab, nft, 64, 4).astype(np.float32))
+
+
+def wino_weights_x3(w: np.ndarray, nslab: int, U: np.ndarray | None = None):
+    """Split-f16 form of wino_weights for idf_conv3x3_wx3 (conv3_wino.hip, X3).
+
+    U = G g G^T in float64, scaled by 2^k (k per layer: max |U| * 2^k in [2^14, 2^15), so
+    the f16 pairs keep full precision down to ~2^-17 of the largest weight), then split
+    Uh = f16(U'), Ul = f16(U' - Uh) (both round-to-nearest-even).  Returns
+    (uint16 [16 positions][nslab][nft][64 lanes][8] = (Uh[4], Ul[4]) of the same lane
+    element order as wino_weights, yscale = 2^-k)."""
+    if U is None:
+        U = wino_transform64(w, nslab)
+    n_alloc = U.shape[1]
+    nft = n_alloc // 16
+    m = float(np.abs(U).max())
+    k = 0 if m == 0.0 else int(np.floor(np.log2(16384.0 / m)))
+    k = max(-14, min(k, 60))
+    Us = U * (2.0 ** k)
+    hi = Us.astype(np.float16)
+    lo = (Us - hi.astype(np.float64)).astype(np.float16)
+    out = np.empty((16, nft, 16, nslab, 4, 2, 4), np.uint16)  # pos, f, r, slab, h, hi/lo, e
+    out[..., 0, :] = hi.view(np.uint16).reshape(16, nft, 16, nslab, 4, 4)
+    out[..., 1, :] = lo.view(np.uint16).reshape(16, nft, 16, nslab, 4, 4)
+    out = out.transpose(0, 3, 1, 4, 2, 5, 6)  # pos, slab, f, h, r, hi/lo, e
+    return np.ascontiguousarray(out.reshape(16, nslab, nft, 64, 8)), float(2.0 ** -k)
 
 
 def bf16_weights(w: np.ndarray, C: int) -> np.ndarray:
@@ -181,7 +216,7 @@ def interior_bias(b3: np.ndarray, v: np.ndarray) -> np.ndarray:
 
 def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
                      slope: float = 0.01, fold: bool = False, wino: bool = False,
-                     bf16: bool = False) -> PackedBlock:
+                     bf16: bool = False, wx3: bool = False) -> PackedBlock:
     """Pack the reference DenseBlock parameters found under `prefix` in `sd`
     (keys `{prefix}layers.{i}.layers.{0,1}.{weight,bias}`, head `{prefix}layers.{depth}.*`).
     fold=True folds each layer's 1x1 conv into its 3x3 conv (fold_layer)."""
@@ -199,7 +234,7 @@ def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
     geom = BlockGeometry(a=a, depth=depth, growth=gs, n_head=n_head)
     g_alloc = round_up(geom.g_pad, tile_n(geom.g_pad))
     w1s, b1s, w3s, b3s, n1s, ld1s, ld3s = [], [], [], [], [], [], []
-    vts, bfs, wus, wbs = [], [], [], []
+    vts, bfs, wus, wbs, wxs, wys = [], [], [], [], [], []
     c = a
     for i in range(depth):
         k = geom.k_in[i]
@@ -227,7 +262,12 @@ def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
             if wino:
                 w64 = np.zeros((g_alloc, 9, ldw3), np.float64)
                 w64[:g][:, :, pos] = wf64
-                wus.append(wino_weights(w64, ldw3 // 16))
+                U64 = wino_transform64(w64, ldw3 // 16)
+                wus.append(wino_weights(w64, ldw3 // 16, U64))
+                if wx3:
+                    ux, ysc = wino_weights_x3(w64, ldw3 // 16, U64)
+                    wxs.append(ux)
+                    wys.append(ysc)
             if bf16:
                 if g_alloc > 48:
                     raise NotImplementedError(
@@ -252,7 +292,7 @@ def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
     bhp = np.zeros(nh_alloc, np.float32)
     bhp[:n_head] = arr(f"layers.{depth}.bias")
     return PackedBlock(geom, act, slope, fold, vts, bfs, w1s, b1s, w3s, b3s, whp, bhp, g_alloc,
-                       n1s, ld1s, ld3s, nh_alloc, ldwh, wus, wbs)
+                       n1s, ld1s, ld3s, nh_alloc, ldwh, wus, wbs, wxs, wys)
 
 
 def unpack_features(feat: np.ndarray, geom: BlockGeometry, n: int) -> np.ndarray:

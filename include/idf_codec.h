@@ -169,6 +169,14 @@ typedef struct IdfDenseBlock {
    * fragment-ordered bf16 weights wb16[i] -- for configs that name bf16 coupling convs */
   int32_t bf16;
   const uint16_t *wb16[IDF_MAX_DEPTH];
+  /* wx3 = 1 (with wino = 1): layers with wx3_u[i] run the split-f16 Winograd conv
+   * (idf_conv3x3_wx3) with yscale wx3_yscale[i]; layer 0 range-checks its input (the block
+   * input), every layer its outputs, OR-ing 1 into *range_flag (device, may be NULL) when the
+   * guard trips -- the caller then recomputes with wx3 = 0 (exact-f32 Winograd) */
+  int32_t wx3;
+  float wx3_yscale[IDF_MAX_DEPTH];
+  const uint16_t *wx3_u[IDF_MAX_DEPTH];
+  uint32_t *range_flag;
 } IdfDenseBlock;
 
 /* Head epilogue target */
@@ -268,6 +276,30 @@ int idf_conv3x3_wino_res(void *stream, int32_t B, int32_t H, int32_t W, int32_t 
                          const float *d_bias, int32_t N, float *d_out, int64_t ld_out,
                          const float *d_res, int64_t ld_res, int32_t act, float slope,
                          float *d_workspace, int64_t workspace_floats);
+
+/* The same Winograd convs with fp32-accurate split-f16 products ("wx3"): every transformed
+ * input V and weight U' = U * 2^k is carried as an f16 pair (hi + lo) and V.U' is summed as
+ * Vl.Uh + Vh.Ul + Vh.Uh on v_mfma_f32_16x16x16_f16 with f32 accumulation (each f16 x f16
+ * product is exact in f32; the dropped Vl.Ul term is ~2^-22 relative), then scaled by
+ * yscale = 2^-k.  d_u: uint16 [16 positions][ceil(C/16) slabs][nft][64 lanes][hi 4, lo 4]
+ * (idfcodec/packing.py wino_weights_x3), the same bytes per weight as the fp32 layout.
+ * Range guard (d_flag may be NULL): the kernel ORs 1 into *d_flag if any stored output has
+ * |y| >= 8192 or is NaN, or -- with check_input != 0 -- any transformed input has |V| >= 32768
+ * or the input holds a NaN.  |V| <= 4 max |x|, so inputs that are outputs of guarded convs
+ * need no input check (a DenseBlock checks only its first layer).  On a set flag the caller
+ * recomputes with the exact-f32 kernel.  Same geometry/workspace rules. */
+int idf_conv3x3_wx3(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, const float *d_x,
+                    int64_t ld_x, const uint16_t *d_u, int32_t nft, float yscale,
+                    const float *d_b3, const float *d_vtap, int32_t ldv, const float *d_bfull,
+                    int32_t N, float *d_out, int64_t ld_out, int32_t act, float slope,
+                    uint32_t *d_flag, int32_t check_input, float *d_workspace,
+                    int64_t workspace_floats);
+int idf_conv3x3_wx3_res(void *stream, int32_t B, int32_t H, int32_t W, int32_t C,
+                        const float *d_x, int64_t ld_x, const uint16_t *d_u, int32_t nft,
+                        float yscale, const float *d_bias, int32_t N, float *d_out,
+                        int64_t ld_out, const float *d_res, int64_t ld_res, int32_t act,
+                        float slope, uint32_t *d_flag, int32_t check_input,
+                        float *d_workspace, int64_t workspace_floats);
 
 /* The same folded 3x3 conv on bf16 MFMA (v_mfma_f32_16x16x32_bf16, fp32 accumulation).
  * The input is the bf16 shadow d_x16 of the fp32 feature columns (ld_x16 a multiple of 8,

@@ -306,3 +306,17 @@ def test_bf16_weight_packing_layout():
                 c = 32 * s + 8 * kb + e
                 want = ref[:, :, c] if c < C else np.zeros((n_alloc, 9), np.float32)
                 assert np.array_equal(back[s, :, kb, :, e].T, want)
+
+
+def test_bitstream_conv_flag_round_trips():
+    import torch
+    from idfcodec.codec import Bitstream
+    st = torch.tensor([1 << 32, 5], dtype=torch.int64)
+    nw = torch.tensor([1, 2], dtype=torch.int64)
+    w = torch.tensor([7, 8, 9], dtype=torch.int32)
+    for mode in ("x3", "f32"):
+        bs = Bitstream(1, [(6, 4, 4), (12, 2, 2)], st, nw, w, meta={"n_subpixels": 48, "conv": mode})
+        back = Bitstream.from_bytes(bs.to_bytes())
+        assert back.meta["conv"] == mode
+    legacy = Bitstream(1, [(6, 4, 4), (12, 2, 2)], st, nw, w)  # written before the flag
+    assert Bitstream.from_bytes(legacy.to_bytes()).meta["conv"] == "f32"

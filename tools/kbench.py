@@ -33,7 +33,7 @@ def main():
     dev = torch.device("cuda")
     s = _lib.stream_ptr()
     g_pad, g_alloc, g_real = 44, 48, 43
-    only = os.environ.get("KB_ONLY", "wino,halo,gemm,bf16").split(",")
+    only = os.environ.get("KB_ONLY", "wino,wx3,halo,gemm,bf16").split(",")
     layers = [int(v) for v in os.environ.get("KB_LAYERS", "0,3,6,9,11").split(",")]
     levels = [int(v) for v in os.environ.get("KB_LEVELS", "0,1,2").split(",")]
     reps = int(os.environ.get("KB_REPS", "10"))
@@ -72,6 +72,18 @@ def main():
                                              ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
                                              ptr(feat) + c_pad * 4, ld, 0, 0.0, ptr(wws), wwn), "wino")
 
+            from idfcodec.packing import wino_weights_x3
+            UX, ysc = wino_weights_x3(np.random.default_rng(0).normal(
+                0, 0.01, (g_alloc, 9, ldw)), ldw // 16)
+            UX = torch.from_numpy(UX.view(np.int16)).to(dev)
+            flag = torch.zeros(1, dtype=torch.int32, device=dev)
+
+            def wx3():
+                check(lib().idf_conv3x3_wx3(s, B, hw, hw, c_pad, ptr(feat), ld, ptr(UX), g_alloc // 16,
+                                            ysc, ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
+                                            ptr(feat) + c_pad * 4, ld, 0, 0.0, ptr(flag), 0, ptr(wws),
+                                            wwn), "wx3")
+
             from idfcodec.packing import bf16_weights
             WB = torch.from_numpy(bf16_weights(np.random.default_rng(1).normal(
                 0, 0.01, (g_alloc, 9, ldw)).astype(np.float32), c_pad).view(np.int16)).to(dev)
@@ -93,7 +105,7 @@ def main():
                                                  g_alloc, ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
                                                  ptr(feat) + c_pad * 4, ld, 0, 0.0), "gemm")
             line = f"L{lvl} hw={hw:2d} c={c_pad:4d} P={P:7d}"
-            for name, fn in (("wino", wino), ("halo", halo), ("gemm", gemm), ("bf16", bf16)):
+            for name, fn in (("wino", wino), ("wx3", wx3), ("halo", halo), ("gemm", gemm), ("bf16", bf16)):
                 if name not in only:
                     continue
                 ms = time_it(fn, reps)

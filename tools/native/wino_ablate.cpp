@@ -16,7 +16,10 @@ static float* dev_random(size_t n) {
   return d;
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const bool x3 = argc > 1 && argv[1][0] == 'x';
+  uint32_t* flag;
+  if (hipMalloc(&flag, 4) != hipSuccess) abort();
   struct Case { int B, hw, c; } cases[] = {{256, 32, 496}, {256, 16, 504}, {256, 8, 520}};
   const int N = 44, n_alloc = 48;
   for (auto& cs : cases) {
@@ -25,15 +28,20 @@ int main() {
     float* U = dev_random((size_t)16 * nslab * (n_alloc / 16) * 256);
     float* b = dev_random(n_alloc * 10);
     const int64_t wsn = idf_conv3x3_wino_workspace(cs.B, cs.hw, cs.hw, cs.c, N);
-    float* ws = wsn ? dev_random(wsn) : nullptr;
+    const int64_t nblk_dbg = (int64_t)cs.B * cs.hw * cs.hw / 64 * 8 * 4 + 4096;
+    float* ws = (wsn || IDF_WINO_STAMPS) ? dev_random(wsn > nblk_dbg ? wsn : nblk_dbg) : nullptr;
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     float best = 1e9f;
     for (int rep = 0; rep < 6; ++rep) {
       (void)hipEventRecord(e0, 0);
-      int rc = idf_conv3x3_wino(nullptr, cs.B, cs.hw, cs.hw, cs.c, X, ld, U, n_alloc / 16, b, b + n_alloc,
-                                n_alloc, b + 8 * n_alloc, N, X + cs.c, ld, 1, 0.f, ws, wsn);
+      int rc = x3 ? idf_conv3x3_wx3(nullptr, cs.B, cs.hw, cs.hw, cs.c, X, ld, (const uint16_t*)U,
+                                    n_alloc / 16, 1.0f, b, b + n_alloc, n_alloc, b + 8 * n_alloc, N,
+                                    X + cs.c, ld, 1, 0.f, flag, 0, ws, wsn)
+                  : idf_conv3x3_wino(nullptr, cs.B, cs.hw, cs.hw, cs.c, X, ld, U, n_alloc / 16, b,
+                                     b + n_alloc, n_alloc, b + 8 * n_alloc, N, X + cs.c, ld, 1, 0.f,
+                                     ws, wsn);
       (void)hipEventRecord(e1, 0);
       (void)hipEventSynchronize(e1);
       if (rc) { printf("rc=%d\n", rc); return 1; }
@@ -41,8 +49,20 @@ int main() {
       (void)hipEventElapsedTime(&ms, e0, e1);
       if (rep && ms < best) best = ms;
     }
+    if (IDF_WINO_STAMPS && x3 && wsn == 0) {
+      std::vector<float> h((size_t)nblk_dbg);
+      (void)hipMemcpy(h.data(), ws, nblk_dbg * 4, hipMemcpyDeviceToHost);
+      const int nb = cs.B * cs.hw * cs.hw / 256;
+      double sw = 0, si = 0, st = 0;
+      for (int b = 0; b < nb; ++b)
+        for (int w = 0; w < 8; ++w) {
+          sw += h[(b * 8 + w) * 4]; si += h[(b * 8 + w) * 4 + 1]; st += h[(b * 8 + w) * 4 + 2];
+        }
+      printf("  stamps (memtime units/wave): loop %.0f  barrier-wait %.0f  dma-issue %.0f\n",
+             st / nb / 8, sw / nb / 8, si / nb / 8);
+    }
     const double mfma = 2.0 * cs.B * (cs.hw / 2) * (cs.hw / 2) * 16 * (nslab * 16.0) * n_alloc;
-    printf("ablate=%d hw=%d c=%d: %.1f us  executed-MFMA %.1f TF/s\n", IDF_WINO_ABLATE, cs.hw, cs.c,
+    printf("%s ablate=%d hw=%d c=%d: %.1f us  executed-MFMA %.1f TF/s\n", x3 ? "x3 " : "f32", IDF_WINO_ABLATE, cs.hw, cs.c,
            best * 1e3, mfma / best / 1e9);
     (void)hipFree(X); (void)hipFree(U); (void)hipFree(b); if (ws) (void)hipFree(ws);
   }
