@@ -51,6 +51,11 @@
 #ifndef IDF_WINO_SCHED
 #define IDF_WINO_SCHED 2
 #endif
+// X3 loop: 1 = halo and U staged through registers with coalesced loads (run_x3r),
+// 0 = both by LDS-DMA (run_x3).
+#ifndef IDF_X3_REGSTAGE
+#define IDF_X3_REGSTAGE 1
+#endif
 
 namespace idf {
 
@@ -347,7 +352,8 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   constexpr bool PIPE = X3 && SLOTS == kWSlots;
   constexpr int USTAGE = 16 * NF * 256;
   constexpr int DMA_SINK = 2 * STAGE + 2 * USTAGE;  // PIPE: 1 KiB target of idle DMA pieces
-  constexpr int LOOP_LDS = PIPE ? DMA_SINK + 256 : 2 * STAGE;
+  constexpr bool REGS = PIPE && IDF_X3_REGSTAGE;  // halo and U through registers (run_x3r)
+  constexpr int LOOP_LDS = PIPE && !REGS ? DMA_SINK + 256 : 2 * STAGE;
   __shared__ __attribute__((aligned(16))) float lds[LOOP_LDS > MS + BT ? LOOP_LDS : MS + BT];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -697,8 +703,147 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
       o[2] = (float)(__builtin_amdgcn_s_memtime() - st_t0);
     }
   };
+  // X3 loop with register staging.  An LDS-DMA piece writes 64 consecutive 16-B LDS slots, so
+  // in the quad-major halo image ([channel quad][slot]) each piece gathers 16 B from each of
+  // 64 pixels: 64 cache lines per 1 KiB.  Here a global load's 64 lanes cover the 4 quads of
+  // 16 pixels instead -- 16 full 64-B lines -- and ds_write_b128 scatters them into the
+  // image (lanes 8k..8k+7 share a quad: conflict-free).  U comes by plain buffer loads
+  // straight into registers, so with no LDS-DMA in flight the compiler's counted vmcnt
+  // waits stay exact.  Per slab s (steps 0..3, barrier at the start of step 2):
+  //   step 0: U(s+1) -> unxt;  step 1: halo(s+1) registers -> stage (s+1)%2 (free since the
+  //   previous barrier: slab s-1's reads ended in its step 1);  step 2: barrier, then the
+  //   loads of halo(s+2) into the staging registers.
+  constexpr int XR_PER_W = (kWMaxHalo + 16 * 8 - 1) / (16 * 8);  // 16 slots x 4 quads / load
+  uint32_t hsrc[XR_PER_W];
+  int hdst[XR_PER_W];
+  if constexpr (REGS) {
+    const int sl = (lane & 7) + 8 * (lane >> 5), hq = (lane >> 3) & 3;
+#pragma unroll
+    for (int m = 0; m < XR_PER_W; ++m) {
+      const int slot = 16 * (wave + 8 * m) + sl;
+      hsrc[m] = kWInvalid;
+      hdst[m] = (hq * SLOTS + (slot < SLOTS ? slot : SLOTS - 1)) * 4;  // slots >= NH: unused
+      if (slot < NH) {
+        const int img = slot / (HH * HWp);
+        const int rem = slot - img * HH * HWp;
+        const int hy = rem / HWp, cs = rem - hy * HWp;
+        const int hx = cs < EH ? 2 * cs : 2 * (cs - EH) + 1;
+        const int y = y0 + hy - 1, x = x0 + hx - 1;
+        if (b0 + img < g.B && y >= 0 && y < g.H && x >= 0 && x < g.Wd)
+          hsrc[m] = (uint32_t)(((((int64_t)img * g.H + y) * g.Wd + x) * g.ldx + 4 * hq) * 4);
+      }
+    }
+  }
+  auto load_halo = [&](int slab, w4 (&hb)[XR_PER_W]) {
+    const int c0 = slab * 16;
+    const int hq4 = 4 * ((lane >> 3) & 3);
+#pragma unroll
+    for (int m = 0; m < XR_PER_W; ++m) {
+      const uint32_t off =
+          (hsrc[m] != kWInvalid && c0 + hq4 < g.C) ? hsrc[m] + (uint32_t)c0 * 4u : kWInvalid;
+      hb[m] = __builtin_bit_cast(w4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+    }
+  };
+  auto store_halo = [&](int buf, const w4 (&hb)[XR_PER_W]) {
+#pragma unroll
+    for (int m = 0; m < XR_PER_W; ++m) *(w4*)(lds + buf * STAGE + hdst[m]) = hb[m];
+  };
+  auto load_ur = [&](int slab, w4 (&u)[2][NF]) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int j = 0; j < NF; ++j) {
+        const uint32_t off = (uint32_t)((((int64_t)(2 * wave + q) * g.nslab + slab) * g.nft + nf0 + j) *
+                                            1024 + lane * 16);
+        u[q][j] = __builtin_bit_cast(w4, __builtin_amdgcn_raw_buffer_load_b128(ur, off, 0, 0));
+      }
+  };
+  auto lds_barrier = [&]() {
+    uint64_t t0 = IDF_WINO_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (IDF_WINO_STAMPS) st_wait += __builtin_amdgcn_s_memtime() - t0;
+  };
+  auto run_x3r = [&](auto a_tag, auto bp_tag) {
+    constexpr int A = decltype(a_tag)::value, BP = decltype(bp_tag)::value;
+    const WinoRole<NF, A, BP> role(HWp, EH);
+    w4 ucur[2][NF], unxt[2][NF];
+    w4 d[2][6];
+    h4 hl[2][4];
+    w4 hb[XR_PER_W];
+    if (s_lo >= s_hi) return;
+    if (IDF_WINO_STAMPS) st_t0 = __builtin_amdgcn_s_memtime();
+    load_halo(s_lo, hb);
+    load_ur(s_lo, ucur);
+    store_halo(0, hb);
+    load_halo(s_lo + 1, hb);
+    lds_barrier();
+    role.fetch(lds + lq * SLOTS * 4, tbase[0], d[0]);
+    role.fetch(lds + lq * SLOTS * 4, tbase[1], d[1]);
+    {
+      w4 v0, v1;
+      role.transform(d[0], v0, v1);
+      role.template split_pair<CHK>(v0, v1, hl[0], gmax, true);
+    }
+    for (int s = s_lo; s < s_hi; ++s) {
+      const int buf = (s - s_lo) & 1;
+      const bool more = s + 1 < s_hi;
+      const float* xq = lds + buf * STAGE + lq * SLOTS * 4;
+      const float* xn = lds + (buf ^ 1) * STAGE + lq * SLOTS * 4;
+      auto step = [&](auto itag) {
+        constexpr int i = decltype(itag)::value;
+        if constexpr (i == 2) {
+          if (!(IDF_WINO_ABLATE & 16)) lds_barrier();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (i == 0 && !(IDF_WINO_ABLATE & 32)) load_ur(s + 1 < s_hi ? s + 1 : s, unxt);
+        if constexpr (i == 1 && !(IDF_WINO_ABLATE & 1)) store_halo(buf ^ 1, hb);
+        if constexpr (i == 2 && !(IDF_WINO_ABLATE & 1)) load_halo(s + 2, hb);
+        {
+          w4 v0, v1;
+          role.transform(d[(i + 1) & 1], v0, v1);
+          role.template split_pair<CHK>(v0, v1, hl[(i + 1) & 1], gmax, i < 3 || more);
+        }
+        if constexpr (i < 2) role.fetch(xq, tbase[i + 2], d[i & 1]);
+        else role.fetch(xn, tbase[i - 2], d[i & 1]);
+        role.mfma_hl(hl[i & 1], ucur, acc[i]);
+        {
+          constexpr int ND = 6;
+          constexpr int nvm = i == 0 ? 2 * NF : (i == 2 ? XR_PER_W : 0);
+          constexpr int nst = i == 1 ? XR_PER_W : 0;
+#pragma unroll
+          for (int k = 0; k < 6 * NF; ++k) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            if (k < ND) {
+              __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+            } else {
+              if (k < ND + nvm) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+              if (k < ND + nst) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      step(std::integral_constant<int, 0>{});
+      step(std::integral_constant<int, 1>{});
+      step(std::integral_constant<int, 2>{});
+      step(std::integral_constant<int, 3>{});
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) ucur[q][j] = unxt[q][j];
+    }
+    lds_barrier();  // every wave done with the stages before the epilogue reuses the LDS
+    if (IDF_WINO_STAMPS && lane == 0 && g.part) {
+      float* o = g.part + ((int64_t)blockIdx.x * 8 + wave) * 4;
+      o[0] = (float)st_wait; o[1] = (float)st_issue;
+      o[2] = (float)(__builtin_amdgcn_s_memtime() - st_t0);
+    }
+  };
   auto go = [&](auto a_tag, auto bp_tag) {
-    if constexpr (PIPE) run_x3(a_tag, bp_tag);
+    if constexpr (REGS) run_x3r(a_tag, bp_tag);
+    else if constexpr (PIPE) run_x3(a_tag, bp_tag);
     else run(a_tag, bp_tag);
   };
   using I0 = std::integral_constant<int, 0>;
