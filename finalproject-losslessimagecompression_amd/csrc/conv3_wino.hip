@@ -56,6 +56,18 @@
 #ifndef IDF_X3_REGSTAGE
 #define IDF_X3_REGSTAGE 1
 #endif
+#ifndef IDF_X3_PRIO
+#define IDF_X3_PRIO 1
+#endif
+// X3 products: 1 = Vl.Uh (K=16) + (Vh.Uh + Vh.Ul) (one K=32 MFMA), 0 = three K=16 MFMAs.
+// Measured no faster (0.91 vs 0.90 ms over the kbench layers), so off.  Note: hipcc (ROCm
+// 7.2) emits NO wait states between a v_mfma_f32_16x16x32_f16 and a following
+// v_mfma_f32_16x16x16_f16 that reads its result as srcC, and the result is wrong
+// (tools/native: mfma_chain_probe); the K=16 -> K=32 order with the batches split by a
+// sched_barrier is the form that passes the parity tests.
+#ifndef IDF_X3_K32
+#define IDF_X3_K32 0
+#endif
 
 namespace idf {
 
@@ -316,6 +328,30 @@ struct WinoRole {
   }
   __device__ __forceinline__ static void mfma_hl(const h4 (&hl)[4], const w4 (&u)[2][NF],
                                                  w4 (&acc)[NF * 2]) {
+    if constexpr (IDF_X3_K32) {
+      // Vl.Uh on v_mfma_f32_16x16x16_f16, then Vh.Uh + Vh.Ul as ONE
+      // v_mfma_f32_16x16x32_f16: k = 8*quad + j takes A = (Vh, Vh) against the lane's
+      // stored B fragment (Uh, Ul) -- two MFMAs instead of three, and the K=32 form runs
+      // ~1.7x the K=16 form's FLOP rate
+      const h8 a0 = __builtin_shufflevector(hl[0], hl[0], 0, 1, 2, 3, 0, 1, 2, 3);
+      const h8 a1 = __builtin_shufflevector(hl[2], hl[2], 0, 1, 2, 3, 0, 1, 2, 3);
+#pragma unroll
+      for (int jn = 0; jn < NF; ++jn) {
+        const h8 ua = __builtin_bit_cast(h8, u[0][jn]), ub = __builtin_bit_cast(h8, u[1][jn]);
+        acc[jn] = __builtin_amdgcn_mfma_f32_16x16x16f16(
+            hl[1], __builtin_shufflevector(ua, ua, 0, 1, 2, 3), acc[jn], 0, 0, 0);
+        acc[NF + jn] = __builtin_amdgcn_mfma_f32_16x16x16f16(
+            hl[3], __builtin_shufflevector(ub, ub, 0, 1, 2, 3), acc[NF + jn], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int jn = 0; jn < NF; ++jn) {
+        const h8 ua = __builtin_bit_cast(h8, u[0][jn]), ub = __builtin_bit_cast(h8, u[1][jn]);
+        acc[jn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, ua, acc[jn], 0, 0, 0);
+        acc[NF + jn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, ub, acc[NF + jn], 0, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int p = 0; p < 3; ++p)
 #pragma unroll
@@ -772,6 +808,9 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
     w4 hb[XR_PER_W];
     if (s_lo >= s_hi) return;
     if (IDF_WINO_STAMPS) st_t0 = __builtin_amdgcn_s_memtime();
+    // the second-dispatched half (waves 4-7) loses every issue arbitration to its older SIMD
+    // partner at equal priority; one static raise evens the two (MI355X_MICROARCH.md)
+    if (IDF_X3_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
     load_halo(s_lo, hb);
     load_ur(s_lo, ucur);
     store_halo(0, hb);
@@ -811,7 +850,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
           constexpr int nvm = i == 0 ? 2 * NF : (i == 2 ? XR_PER_W : 0);
           constexpr int nst = i == 1 ? XR_PER_W : 0;
 #pragma unroll
-          for (int k = 0; k < 6 * NF; ++k) {
+          for (int k = 0; k < (IDF_X3_K32 ? 4 : 6) * NF; ++k) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
             if (k < ND) {
               __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
