@@ -200,20 +200,38 @@ __device__ __forceinline__ int colslot(int j, int EH) { return (j & 1) ? EH + (j
 // The work of a wave whose positions are (A, 2*BP) and (A, 2*BP + 1): per tile-fragment i
 // (16 tiles) six halo reads, the shared B^T row combination and 2 x NF x 4 MFMAs.
 // xq: this lane's channel quad of a stage's halo image ([4 quads][SLOTS][4 floats]).
-template <int NF, int A, int BP>
+// TWC > 0: the output tile width is a compile-time constant, so the six halo offsets of a
+// role are too and fold into the ds_read immediates (no address VALU in the X3 loop).
+template <int NF, int A, int BP, int TWC = 0>
 struct WinoRole {
   using RA = BT<A>;
   using C0 = BT<2 * BP>;
   using C1 = BT<2 * BP + 1>;
   // the three halo columns the pair needs: {0,1,2} (BP=0) or {1,2,3} (BP=1)
   static constexpr int j0 = BP, j1 = BP + 1, j2 = BP + 2;
+  static constexpr int HWc = TWC + 2, EHc = HWc / 2;
+  static constexpr int csc(int j) { return (j & 1) ? EHc + (j >> 1) : (j >> 1); }
+  static constexpr int oc(int e) {
+    return ((e < 3 ? RA::i0 : RA::i1) * HWc + csc(e % 3 == 0 ? j0 : (e % 3 == 1 ? j1 : j2))) * 4;
+  }
   int o[6];
 
   __device__ __forceinline__ WinoRole(int HWp, int EH) {
-    const int r0 = RA::i0 * HWp, r1 = RA::i1 * HWp;
-    const int cs0 = colslot(j0, EH), cs1 = colslot(j1, EH), cs2 = colslot(j2, EH);
-    o[0] = (r0 + cs0) * 4; o[1] = (r0 + cs1) * 4; o[2] = (r0 + cs2) * 4;
-    o[3] = (r1 + cs0) * 4; o[4] = (r1 + cs1) * 4; o[5] = (r1 + cs2) * 4;
+    if constexpr (TWC == 0) {
+      const int r0 = RA::i0 * HWp, r1 = RA::i1 * HWp;
+      const int cs0 = colslot(j0, EH), cs1 = colslot(j1, EH), cs2 = colslot(j2, EH);
+      o[0] = (r0 + cs0) * 4; o[1] = (r0 + cs1) * 4; o[2] = (r0 + cs2) * 4;
+      o[3] = (r1 + cs0) * 4; o[4] = (r1 + cs1) * 4; o[5] = (r1 + cs2) * 4;
+    }
+  }
+
+  // P = this lane's tile base in the stage (quad image + 4 * tile slot)
+  __device__ __forceinline__ void fetch_p(const float* P, w4 (&dd)[6]) const {
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+      if constexpr (TWC > 0) dd[e] = *(const w4*)(P + oc(e));
+      else dd[e] = *(const w4*)(P + o[e]);
+    }
   }
 
   __device__ __forceinline__ void fetch(const float* xq, int tb, w4 (&dd)[6]) const {
@@ -376,7 +394,7 @@ struct WinoRole {
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-template <int NF, int SLOTS, bool X3, bool CHK = false>
+template <int NF, int SLOTS, bool X3, bool CHK = false, int TWC = 0>
 __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   // one stage = the slab's halo image [4 quads][SLOTS][4 floats]
   constexpr int STAGE = 4 * SLOTS * 4;
@@ -801,8 +819,12 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   };
   auto run_x3r = [&](auto a_tag, auto bp_tag) {
     constexpr int A = decltype(a_tag)::value, BP = decltype(bp_tag)::value;
-    const WinoRole<NF, A, BP> role(HWp, EH);
-    w4 ucur[2][NF], unxt[2][NF];
+    const WinoRole<NF, A, BP, TWC> role(HWp, EH);
+    // per tile fragment, this lane's base in stage 0 (stage 1 = + STAGE, a constant offset)
+    const float* pb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pb[i] = lds + lq * SLOTS * 4 + tbase[i] * 4;
+    w4 ua[2][NF], ub[2][NF];  // U of this slab / the next
     w4 d[2][6];
     h4 hl[2][4];
     w4 hb[XR_PER_W];
@@ -812,29 +834,30 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
     // partner at equal priority; one static raise evens the two (MI355X_MICROARCH.md)
     if (IDF_X3_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
     load_halo(s_lo, hb);
-    load_ur(s_lo, ucur);
+    load_ur(s_lo, ua);
     store_halo(0, hb);
     load_halo(s_lo + 1, hb);
     lds_barrier();
-    role.fetch(lds + lq * SLOTS * 4, tbase[0], d[0]);
-    role.fetch(lds + lq * SLOTS * 4, tbase[1], d[1]);
+    role.fetch_p(pb[0], d[0]);
+    role.fetch_p(pb[1], d[1]);
     {
       w4 v0, v1;
       role.transform(d[0], v0, v1);
       role.template split_pair<CHK>(v0, v1, hl[0], gmax, true);
     }
+    w4 (&ucur)[2][NF] = ua;
+    w4 (&unxt)[2][NF] = ub;
     for (int s = s_lo; s < s_hi; ++s) {
       const int buf = (s - s_lo) & 1;
       const bool more = s + 1 < s_hi;
-      const float* xq = lds + buf * STAGE + lq * SLOTS * 4;
-      const float* xn = lds + (buf ^ 1) * STAGE + lq * SLOTS * 4;
+      const int qoff = buf * STAGE, noff = (buf ^ 1) * STAGE;  // uniform stage offsets
       auto step = [&](auto itag) {
         constexpr int i = decltype(itag)::value;
         if constexpr (i == 2) {
           if (!(IDF_WINO_ABLATE & 16)) lds_barrier();
         }
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (i == 0 && !(IDF_WINO_ABLATE & 32)) load_ur(s + 1 < s_hi ? s + 1 : s, unxt);
+        if constexpr (i == 0 && !(IDF_WINO_ABLATE & 32)) load_ur(more ? s + 1 : s, unxt);
         if constexpr (i == 1 && !(IDF_WINO_ABLATE & 1)) store_halo(buf ^ 1, hb);
         if constexpr (i == 2 && !(IDF_WINO_ABLATE & 1)) load_halo(s + 2, hb);
         {
@@ -842,8 +865,9 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
           role.transform(d[(i + 1) & 1], v0, v1);
           role.template split_pair<CHK>(v0, v1, hl[(i + 1) & 1], gmax, i < 3 || more);
         }
-        if constexpr (i < 2) role.fetch(xq, tbase[i + 2], d[i & 1]);
-        else role.fetch(xn, tbase[i - 2], d[i & 1]);
+        // the halo offsets are immediates (TWC > 0): one address add per fetch
+        if constexpr (i < 2) role.fetch_p(pb[i + 2] + qoff, d[i & 1]);
+        else role.fetch_p(pb[i - 2] + noff, d[i & 1]);
         role.mfma_hl(hl[i & 1], ucur, acc[i]);
         {
           constexpr int ND = 6;
@@ -1135,10 +1159,18 @@ static int wino_launch(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
     if (x3) IDF_WINO_NF(kWSlotsBig, true, false) else IDF_WINO_NF(kWSlotsBig, false, false)
   } else if (!x3) {
     IDF_WINO_NF(kWSlots, false, false)
-  } else if (check_in) {
-    IDF_WINO_NF(kWSlots, true, true)
   } else {
-    IDF_WINO_NF(kWSlots, true, false)
+#define IDF_WX3_TW(chk, twc)                                                                   \
+  hipLaunchKernelGGL((conv3_wino_kernel<3, kWSlots, true, chk, twc>), dim3((unsigned)blocks),   \
+                     dim3(kWThreads), 0, s, g)
+    // the common tile widths (imagenet64: 32, 16, 8) with compile-time halo offsets
+    const int twc = NF == 3 && (pl.TW == 32 || pl.TW == 16 || pl.TW == 8) ? pl.TW : 0;
+    if (twc == 32) { if (check_in) IDF_WX3_TW(true, 32); else IDF_WX3_TW(false, 32); }
+    else if (twc == 16) { if (check_in) IDF_WX3_TW(true, 16); else IDF_WX3_TW(false, 16); }
+    else if (twc == 8) { if (check_in) IDF_WX3_TW(true, 8); else IDF_WX3_TW(false, 8); }
+    else if (check_in) IDF_WINO_NF(kWSlots, true, true)
+    else IDF_WINO_NF(kWSlots, true, false)
+#undef IDF_WX3_TW
   }
 #undef IDF_WINO_NF
 #undef IDF_WINO_LAUNCH
