@@ -31,6 +31,7 @@
 // into partial Y tiles that conv3_wino_reduce_kernel sums in fixed order.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -515,6 +516,12 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
     tbase[i] = (img * HH + 2 * ty) * HWp + tx;
   }
 
+  // REGS: the epilogue's bias table lies past the halo stages, so stage it now (its global
+  // loads' latency hides under the main loop; the loop's barriers publish it)
+  if constexpr (REGS) {
+    if (g.ksplit == 1)
+      stage_bias(lds + MS, NF * 16, nf0 * 16, g.N, g.b3, g.vtap, g.bfull, g.ldv, tid, kWThreads);
+  }
   w4 acc[4][2 * NF];  // [tile fragment][position q * NF + n-fragment]
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -938,39 +945,92 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   }
 
   bool out_ok = true;  // X3: every stored output within kX3OutGuard (false on NaN)
+  const uint64_t st_epi = IDF_WINO_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
 
+  // LDS-only barrier for the epilogue: __syncthreads() would also drain every global store
+  // issued so far (vmcnt(0)), exposing the store latency once per n-fragment
+  auto epi_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  // the two output tiles this thread finishes (the same for every n-fragment): image, the
+  // 2x2 pixels as indices relative to the block's first image (-1 outside the image / batch)
+  // and their border classes -- the divisions and 64-bit address math done once
+  int e_img[2], e_q[2][2][2], e_cls[2][2][2];
+  const int64_t pix0 = (int64_t)b0 * g.H * g.Wd;
+  float* obase = g.out ? g.out + pix0 * g.ldo : nullptr;
+  float* pbase = g.part ? g.part + ((int64_t)ks * ((int64_t)g.B * g.H * g.Wd) + pix0) * g.ldp : nullptr;
+  const float* rbase = g.res ? g.res + pix0 * g.ldr : nullptr;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int t = (tid + kWThreads * it) >> 4;
+    const int img = t / TPI;
+    const int rem = t - img * TPI;
+    const int ty = rem / TTW, tx = rem - ty * TTW;
+    e_img[it] = img;
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int y = y0 + 2 * ty + r, x = x0 + 2 * tx + c;
+        const bool ok = img < g.IMGS && b0 + img < g.B && y < g.H && x < g.Wd;
+        e_q[it][r][c] = ok ? (img * g.H + y) * g.Wd + x : -1;
+        e_cls[it][r][c] = bias_class(y, x, g.H, g.Wd);
+      }
+  }
+  uint64_t st_e[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (IDF_WINO_STAMPS) st_e[0] = __builtin_amdgcn_s_memtime();
   // ---- output transform, one n-fragment at a time through LDS
-  float* Ms = lds;  // [16 pos][64 tiles][kWMsPitch]
+  float* Ms = lds;  // [16 pos][64 tiles][kWMsPitch]; REGS: [16 n][64 tiles][16 pos] (+4 per n)
   float* btab = lds + MS;  // [16 border classes][NF * 16]
-  if (g.ksplit == 1) stage_bias(btab, NF * 16, nf0 * 16, g.N, g.b3, g.vtap, g.bfull, g.ldv, tid, kWThreads);
+  constexpr int ERW = 64 * 16 + 4;  // REGS staging: floats per n row (16-B pad: b64 writes,
+                                    // b128 reads at most 2-way conflicted)
+  static_assert(!REGS || 16 * ERW <= MS, "REGS staging must fit below the bias table");
+  if (g.ksplit == 1 && !REGS)
+    stage_bias(btab, NF * 16, nf0 * 16, g.N, g.b3, g.vtap, g.bfull, g.ldv, tid, kWThreads);
 #pragma unroll
   for (int j = 0; j < NF; ++j) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int p = 2 * wave + q;
+    if constexpr (REGS) {
+      // a wave's two positions are adjacent: one 8-B write per (tile fragment, row)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int t = 16 * i + (lane >> 4) * 4 + r;
-          Ms[(p * 64 + t) * kWMsPitch + lr] = acc[i][q * NF + j][r];
+          typedef float f2s __attribute__((ext_vector_type(2)));
+          *(f2s*)(Ms + lr * ERW + t * 16 + 2 * wave) = f2s{acc[i][j][r], acc[i][NF + j][r]};
         }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int p = 2 * wave + q;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int t = 16 * i + (lane >> 4) * 4 + r;
+            Ms[(p * 64 + t) * kWMsPitch + lr] = acc[i][q * NF + j][r];
+          }
+      }
     }
-    __syncthreads();
+    epi_barrier();
+    if (IDF_WINO_STAMPS) st_e[1 + 2 * j] = __builtin_amdgcn_s_memtime();
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
-      const int item = tid + kWThreads * it;
-      const int t = item >> 4, nn = item & 15;
-      int img = t / TPI;
-      const int rem = t - img * TPI;
-      const int ty = rem / TTW, tx = rem - ty * TTW;
+      const int t = (tid + kWThreads * it) >> 4, nn = tid & 15;
       const int n = (nf0 + j) * 16 + nn;
-      if (img < g.IMGS && n < g.N) {
+      if (e_img[it] < g.IMGS && n < g.N) {
         float m[4][4];
+        if constexpr (REGS) {
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
+          for (int a = 0; a < 4; ++a) {
+            const w4 row = *(const w4*)(Ms + nn * ERW + t * 16 + 4 * a);
 #pragma unroll
-          for (int b = 0; b < 4; ++b) m[a][b] = Ms[((a * 4 + b) * 64 + t) * kWMsPitch + nn];
+            for (int b = 0; b < 4; ++b) m[a][b] = row[b];
+          }
+        } else {
+#pragma unroll
+          for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) m[a][b] = Ms[((a * 4 + b) * 64 + t) * kWMsPitch + nn];
+        }
         // A^T m: rows (m0 + m1 + m2), (m1 - m2 - m3); then the same over columns
         float u0[4], u1[4];
 #pragma unroll
@@ -989,42 +1049,45 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
 #pragma unroll
             for (int c = 0; c < 2; ++c) Y[r][c] = Y[r][c] * g.yscale;
         }
-        const int b = b0 + img;
         // residual loads for the 2x2 outputs before any of their stores
         float rv[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
         if (g.res && g.ksplit == 1) {
 #pragma unroll
           for (int r = 0; r < 2; ++r)
 #pragma unroll
-            for (int c = 0; c < 2; ++c) {
-              const int y = y0 + 2 * ty + r, x = x0 + 2 * tx + c;
-              if (b < g.B && y < g.H && x < g.Wd)
-                rv[r][c] = g.res[(((int64_t)b * g.H + y) * g.Wd + x) * g.ldr + n];
-            }
+            for (int c = 0; c < 2; ++c)
+              if (e_q[it][r][c] >= 0) rv[r][c] = rbase[(int64_t)e_q[it][r][c] * g.ldr + n];
         }
 #pragma unroll
         for (int r = 0; r < 2; ++r)
 #pragma unroll
           for (int c = 0; c < 2; ++c) {
-            const int y = y0 + 2 * ty + r, x = x0 + 2 * tx + c;
-            if (b >= g.B || y >= g.H || x >= g.Wd) continue;
-            const int64_t p = ((int64_t)b * g.H + y) * g.Wd + x;
+            const int qp = e_q[it][r][c];  // the output pixel relative to the block's first image
+            if (qp < 0) continue;
             if (g.ksplit == 1) {
-              float v = Y[r][c] + btab[bias_class(y, x, g.H, g.Wd) * (NF * 16) + n - nf0 * 16];
+              float v = Y[r][c] + btab[e_cls[it][r][c] * (NF * 16) + n - nf0 * 16];
               if (g.res) v = rv[r][c] + v;
               v = wact(v, g.act, g.slope);
               if constexpr (X3) out_ok = out_ok && fabsf(v) < kX3OutGuard;
-              g.out[p * g.ldo + n] = v;
+              if (!(IDF_WINO_ABLATE & 128)) obase[(int64_t)qp * g.ldo + n] = v;
+              else if (v == 12345.f) obase[0] = v;
             }
             else
-              g.part[((int64_t)ks * ((int64_t)g.B * g.H * g.Wd) + p) * g.ldp + n] = Y[r][c];
+              pbase[(int64_t)qp * g.ldp + n] = Y[r][c];
           }
       }
     }
-    __syncthreads();
+    if (IDF_WINO_STAMPS) st_e[2 + 2 * j] = __builtin_amdgcn_s_memtime();
+    epi_barrier();
   }
   if constexpr (X3) {
     if (!out_ok && g.flag) atomicOr(g.flag, 1u);
+  }
+  if (IDF_WINO_STAMPS && PIPE && lane == 0 && g.part) {
+    g.part[((int64_t)blockIdx.x * 8 + wave) * 4 + 3] = (float)(__builtin_amdgcn_s_memtime() - st_epi);
+    float* dbg = g.part + (int64_t)gridDim.x * 32 + ((int64_t)blockIdx.x * 8 + wave) * 8;
+    dbg[0] = (float)(st_e[0] - st_epi);
+    for (int k = 1; k <= 2 * NF; ++k) dbg[k] = (float)(st_e[k] - st_e[k - 1]);
   }
 }
 
@@ -1087,6 +1150,13 @@ static WinoPlan wino_plan(int H, int W, int nslab, int N) {
   // and reduce then cost more than they gain (measured: config 4 5.4 -> 8.3 Mpx/s, config 3's
   // VQ-VAE 67 -> 54 ms; imagenet64's 8x8 level keeps 4: 10.2 vs 9.6 Mpx/s with 1).
   if (pl.big || N > 64) pl.ksplit = 1;
+  {  // timing experiments only: cap the split (IDF_WINO_KSPLIT_MAX)
+    static const int cap = [] {
+      const char* e = getenv("IDF_WINO_KSPLIT_MAX");
+      return e ? atoi(e) : 0;
+    }();
+    if (cap > 0 && pl.ksplit > cap) pl.ksplit = cap;
+  }
   if (pl.ksplit > nslab) pl.ksplit = nslab > 0 ? nslab : 1;
   pl.ok = 1;
   return pl;

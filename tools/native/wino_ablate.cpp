@@ -20,7 +20,7 @@ int main(int argc, char** argv) {
   const bool x3 = argc > 1 && argv[1][0] == 'x';
   uint32_t* flag;
   if (hipMalloc(&flag, 4) != hipSuccess) abort();
-  struct Case { int B, hw, c; } cases[] = {{256, 32, 496}, {256, 16, 504}, {256, 8, 520}};
+  struct Case { int B, hw, c; } cases[] = {{256, 32, 496}, {256, 16, 504}, {256, 8, 520}, {256, 32, 16}};
   const int N = 44, n_alloc = 48;
   for (auto& cs : cases) {
     const int P = cs.B * cs.hw * cs.hw, ld = (cs.c + N + 15) / 16 * 16, nslab = (cs.c + 15) / 16;
@@ -28,7 +28,7 @@ int main(int argc, char** argv) {
     float* U = dev_random((size_t)16 * nslab * (n_alloc / 16) * 256);
     float* b = dev_random(n_alloc * 10);
     const int64_t wsn = idf_conv3x3_wino_workspace(cs.B, cs.hw, cs.hw, cs.c, N);
-    const int64_t nblk_dbg = (int64_t)cs.B * cs.hw * cs.hw / 64 * 8 * 4 + 4096;
+    const int64_t nblk_dbg = (int64_t)cs.B * cs.hw * cs.hw / 64 * 8 * 12 + 4096;
     float* ws = (wsn || IDF_WINO_STAMPS) ? dev_random(wsn > nblk_dbg ? wsn : nblk_dbg) : nullptr;
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
@@ -53,13 +53,21 @@ int main(int argc, char** argv) {
       std::vector<float> h((size_t)nblk_dbg);
       (void)hipMemcpy(h.data(), ws, nblk_dbg * 4, hipMemcpyDeviceToHost);
       const int nb = cs.B * cs.hw * cs.hw / 256;
-      double sw = 0, si = 0, st = 0;
+      double sw = 0, si = 0, st = 0, se = 0;
       for (int b = 0; b < nb; ++b)
         for (int w = 0; w < 8; ++w) {
           sw += h[(b * 8 + w) * 4]; si += h[(b * 8 + w) * 4 + 1]; st += h[(b * 8 + w) * 4 + 2];
+          se += h[(b * 8 + w) * 4 + 3];
         }
-      printf("  stamps (memtime units/wave): loop %.0f  barrier-wait %.0f  dma-issue %.0f\n",
-             st / nb / 8, sw / nb / 8, si / nb / 8);
+      printf("  stamps (memtime units/wave): loop %.0f  barrier-wait %.0f  dma-issue %.0f  epilogue %.0f\n",
+             st / nb / 8, sw / nb / 8, si / nb / 8, se / nb / 8);
+      double ep[8] = {0};
+      for (int b = 0; b < nb; ++b)
+        for (int w = 0; w < 8; ++w)
+          for (int k = 0; k < 7; ++k) ep[k] += h[(size_t)nb * 32 + (b * 8 + w) * 8 + k];
+      printf("  epilogue phases: pre %.0f | j0 write+bar %.0f  rest %.0f | j1 %.0f %.0f | j2 %.0f %.0f\n",
+             ep[0] / nb / 8, ep[1] / nb / 8, ep[2] / nb / 8, ep[3] / nb / 8, ep[4] / nb / 8,
+             ep[5] / nb / 8, ep[6] / nb / 8);
     }
     const double mfma = 2.0 * cs.B * (cs.hw / 2) * (cs.hw / 2) * 16 * (nslab * 16.0) * n_alloc;
     printf("%s ablate=%d hw=%d c=%d: %.1f us  executed-MFMA %.1f TF/s\n", x3 ? "x3 " : "f32", IDF_WINO_ABLATE, cs.hw, cs.c,
