@@ -404,12 +404,16 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   constexpr int BT = 16 * NF * 16;         // epilogue bias table, after the staging
   // X3 with the standard stage: U also goes through LDS (two [16 pos][NF][64][4] stages after
   // the halo stages) so that the loop holds no ordinary global load -- see run_x3 below.
-  constexpr bool PIPE = X3 && SLOTS == kWSlots;
+  // the pipelined X3 loops; the packed-small-image stage (1024 slots) only with register
+  // staging and NF <= 2 (its 8 halo loads per wave and slab need the registers)
+  constexpr bool PIPE = X3 && (SLOTS == kWSlots || (SLOTS == kWSlotsBig && NF <= 2 && IDF_X3_REGSTAGE));
   constexpr int USTAGE = 16 * NF * 256;
   constexpr int DMA_SINK = 2 * STAGE + 2 * USTAGE;  // PIPE: 1 KiB target of idle DMA pieces
   constexpr bool REGS = PIPE && IDF_X3_REGSTAGE;  // halo and U through registers (run_x3r)
   constexpr int LOOP_LDS = PIPE && !REGS ? DMA_SINK + 256 : 2 * STAGE;
-  __shared__ __attribute__((aligned(16))) float lds[LOOP_LDS > MS + BT ? LOOP_LDS : MS + BT];
+  // REGS stages the epilogue bias table before the main loop: it must lie past the stages
+  constexpr int BT_OFF = REGS && 2 * STAGE > MS ? 2 * STAGE : MS;
+  __shared__ __attribute__((aligned(16))) float lds[LOOP_LDS > BT_OFF + BT ? LOOP_LDS : BT_OFF + BT];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -520,7 +524,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   // loads' latency hides under the main loop; the loop's barriers publish it)
   if constexpr (REGS) {
     if (g.ksplit == 1)
-      stage_bias(lds + MS, NF * 16, nf0 * 16, g.N, g.b3, g.vtap, g.bfull, g.ldv, tid, kWThreads);
+      stage_bias(lds + BT_OFF, NF * 16, nf0 * 16, g.N, g.b3, g.vtap, g.bfull, g.ldv, tid, kWThreads);
   }
   w4 acc[4][2 * NF];  // [tile fragment][position q * NF + n-fragment]
 #pragma unroll
@@ -774,7 +778,8 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   //   step 0: U(s+1) -> unxt;  step 1: halo(s+1) registers -> stage (s+1)%2 (free since the
   //   previous barrier: slab s-1's reads ended in its step 1);  step 2: barrier, then the
   //   loads of halo(s+2) into the staging registers.
-  constexpr int XR_PER_W = (kWMaxHalo + 16 * 8 - 1) / (16 * 8);  // 16 slots x 4 quads / load
+  constexpr int XR_PER_W =  // 16 slots x 4 quads per load
+      ((SLOTS == kWSlotsBig ? kWSlotsBig : kWMaxHalo) + 16 * 8 - 1) / (16 * 8);
   uint32_t hsrc[XR_PER_W];
   int hdst[XR_PER_W];
   if constexpr (REGS) {
@@ -979,10 +984,10 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   if (IDF_WINO_STAMPS) st_e[0] = __builtin_amdgcn_s_memtime();
   // ---- output transform, one n-fragment at a time through LDS
   float* Ms = lds;  // [16 pos][64 tiles][kWMsPitch]; REGS: [16 n][64 tiles][16 pos] (+4 per n)
-  float* btab = lds + MS;  // [16 border classes][NF * 16]
+  float* btab = lds + BT_OFF;  // [16 border classes][NF * 16]
   constexpr int ERW = 64 * 16 + 4;  // REGS staging: floats per n row (16-B pad: b64 writes,
                                     // b128 reads at most 2-way conflicted)
-  static_assert(!REGS || 16 * ERW <= MS, "REGS staging must fit below the bias table");
+  static_assert(!REGS || 16 * ERW <= BT_OFF, "REGS staging must fit below the bias table");
   if (g.ksplit == 1 && !REGS)
     stage_bias(btab, NF * 16, nf0 * 16, g.N, g.b3, g.vtap, g.bfull, g.ldv, tid, kWThreads);
 #pragma unroll
@@ -1226,7 +1231,9 @@ static int wino_launch(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
     default: IDF_WINO_LAUNCH(3, slots, x3, chk); break; \
   }
   if (pl.big) {
-    if (x3) IDF_WINO_NF(kWSlotsBig, true, false) else IDF_WINO_NF(kWSlotsBig, false, false)
+    if (!x3) IDF_WINO_NF(kWSlotsBig, false, false)
+    else if (check_in) IDF_WINO_NF(kWSlotsBig, true, true)
+    else IDF_WINO_NF(kWSlotsBig, true, false)
   } else if (!x3) {
     IDF_WINO_NF(kWSlots, false, false)
   } else {
