@@ -92,7 +92,7 @@ struct EncSym {
 
 __global__ void __launch_bounds__(256) rans_encode_prep_kernel(
     int64_t n, const float* __restrict__ x, const float* __restrict__ mean,
-    const float* __restrict__ scale, EncSym* __restrict__ sym, double* __restrict__ rcp) {
+    const float* __restrict__ scale, EncSym* __restrict__ sym, uint64_t* __restrict__ rcp) {
   __shared__ uint64_t tab[32];
   if (threadIdx.x < 32) tab[threadIdx.x] = kExp2fTab[threadIdx.x];
   __syncthreads();
@@ -100,14 +100,16 @@ __global__ void __launch_bounds__(256) rans_encode_prep_kernel(
   if (i >= n) return;
   float xi = x[i], mi = mean[i], si = scale[i];
   EncSym e = {0, IDF_FREQ_SCALE_ZERO, 0, 0};
-  double r = 0.0;
+  uint64_t r = 0;
   const int lo = rans_lower_int(mi);
   if (si != 0.0f) {  // ZeroDivisionError("float division"), rans.cpp:1435-1438
     float lower = rans_lower_f(lo);  // rans.pyx:51
     float xm = (float)((double)xi - 1.0 / 256.0);
     e.start = rans_cdf(xm, mi, si, lower, tab);      // rans.pyx:52
     e.freq = rans_cdf(xi, mi, si, lower, tab) - e.start;  // rans.pyx:53
-    if (e.freq >= 1 && e.freq <= (1 << 24)) r = 1.0 / (double)(uint32_t)e.freq;
+    // the divisor as the reference widens it (vector<ull>.push_back(int))
+    const uint64_t f = (uint64_t)(int64_t)e.freq;
+    if (f != 0) r = ~0ull / f;
   }
   int32_t f = 0;
   window_check(xi, lo, &f);
@@ -116,93 +118,127 @@ __global__ void __launch_bounds__(256) rans_encode_prep_kernel(
   rcp[i] = r;
 }
 
-// Exact q = state / f, r = state % f for f in [1, 2^24], state < 2^64 with q < 2^40
-// (guaranteed after renormalisation).  The double estimate is within +-1.
-__device__ __forceinline__ void divmod_u64_u24(uint64_t state, uint32_t f, double rcp, uint64_t& q,
-                                               uint64_t& r) {
-  uint64_t qe = (uint64_t)((double)state * rcp);
-  int64_t rr = (int64_t)(state - qe * (uint64_t)f);
-  if (rr < 0) {
-    qe -= 1;
-    rr += f;
-  } else if (rr >= (int64_t)f) {
+// High 64 bits of a 64x64-bit product from 32-bit pieces (uniform operands: SALU
+// s_mul_i32 / s_mul_hi_u32 and carry adds).
+__device__ __forceinline__ uint64_t mulhi_u64(uint64_t a, uint64_t b) {
+  const uint32_t al = (uint32_t)a, ah = (uint32_t)(a >> 32);
+  const uint32_t bl = (uint32_t)b, bh = (uint32_t)(b >> 32);
+  const uint64_t ll = (uint64_t)al * bl, lh = (uint64_t)al * bh;
+  const uint64_t hl = (uint64_t)ah * bl, hh = (uint64_t)ah * bh;
+  const uint64_t mid = (ll >> 32) + (uint32_t)lh + (uint32_t)hl;
+  return hh + (lh >> 32) + (hl >> 32) + (mid >> 32);
+}
+
+// a >= b on 32-bit halves (keeps uniform compares on the scalar unit)
+__device__ __forceinline__ bool ge_u64(uint64_t a, uint64_t b) {
+  const uint32_t ah = (uint32_t)(a >> 32), bh = (uint32_t)(b >> 32);
+  return ah != bh ? ah > bh : (uint32_t)a >= (uint32_t)b;
+}
+
+// Exact q = state / f, r = state % f for any f >= 1, state < 2^64, given
+// m = floor((2^64 - 1) / f): m*f = 2^64 - 1 - rho (0 <= rho < f), so
+// state*m / 2^64 lies in (state/f - 1, state/f] and mulhi(state, m) is q or q - 1.
+__device__ __forceinline__ void divmod_u64_magic(uint64_t state, uint64_t f, uint64_t m,
+                                                 uint64_t& q, uint64_t& r) {
+  uint64_t qe = mulhi_u64(state, m);
+  uint64_t rr = state - qe * f;
+  if (ge_u64(rr, f)) {
     qe += 1;
     rr -= f;
   }
   q = qe;
-  r = (uint64_t)rr;
+  r = rr;
 }
 
-// Pass 2, one lane per stream (rans.pyx:61-66).  Symbol records are loaded kEncAhead
-// symbols ahead of the state chain so the chain never waits on memory.
-constexpr int kEncAhead = 8;
-
+// Pass 2 (rans.pyx:61-66), one wave per stream.  The wave loads the records of 64 symbols
+// at a time with coalesced 16-B + 8-B loads (the next 64 in flight), and the state chain
+// runs on wave-uniform values -- v_readlane of symbol u's record into SGPRs, then scalar
+// arithmetic -- so a symbol costs a few dozen scalar instructions instead of a lane's
+// dependent 64-bit VALU chain.  Emitted words collect in one VGPR (lane = the
+// fill index, one select) and leave as coalesced 256-B stores.
 __global__ void __launch_bounds__(64) rans_encode_kernel(
     int64_t nstreams, const int64_t* __restrict__ sym_off, const EncSym* __restrict__ sym,
-    const double* __restrict__ rcp, const uint64_t* __restrict__ init_state,
+    const uint64_t* __restrict__ magic, const uint64_t* __restrict__ init_state,
     uint64_t* __restrict__ final_state, uint32_t* __restrict__ words, int64_t* __restrict__ nwords,
     int32_t* __restrict__ status) {
-  int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t k = blockIdx.x;
   if (k >= nstreams) return;
+  const int lane = threadIdx.x;
   const int64_t b = sym_off[k], e = sym_off[k + 1];
   uint64_t state = init_state[k];
   uint32_t* out = words + b;
-  int64_t nw = 0;
-  int32_t flag = 0;
-  EncSym cur[kEncAhead], nxt[kEncAhead];
-  double rc_cur[kEncAhead], rc_nxt[kEncAhead];
-  auto load = [&](int64_t i0, EncSym (&sv)[kEncAhead], double (&rv)[kEncAhead]) {
-#pragma unroll
-    for (int u = 0; u < kEncAhead; ++u) {
-      if (i0 + u < e) {
-        sv[u] = sym[i0 + u];
-        rv[u] = rcp[i0 + u];
-      }
+  int64_t nw = 0;  // words stored
+  int fill = 0;    // words waiting in wbuf (lanes 0..fill-1)
+  uint32_t wbuf = 0;
+  int32_t wflag = 0, stop = 0;
+  EncSym cur = {0, 0, 0, 0};
+  uint64_t mcur = 0;
+  if (b + lane < e) {
+    cur = sym[b + lane];
+    mcur = magic[b + lane];
+  }
+  for (int64_t i0 = b; i0 < e; i0 += 64) {
+    EncSym nxt = {0, 0, 0, 0};
+    uint64_t mnxt = 0;
+    if (i0 + 64 + lane < e) {
+      nxt = sym[i0 + 64 + lane];
+      mnxt = magic[i0 + 64 + lane];
     }
-  };
-  load(b, cur, rc_cur);
-  bool stop = false;
-  for (int64_t i0 = b; i0 < e && !stop; i0 += kEncAhead) {
-    if (i0 + kEncAhead < e) load(i0 + kEncAhead, nxt, rc_nxt);
-#pragma unroll
-    for (int u = 0; u < kEncAhead; ++u) {
-      if (i0 + u >= e) break;
-      const int32_t st = cur[u].start, fr = cur[u].freq;
+    const int cnt = (int)(e - i0 < 64 ? e - i0 : 64);
+    const uint32_t mlo_v = (uint32_t)mcur, mhi_v = (uint32_t)(mcur >> 32);
+    int u = 0;
+    for (; u < cnt; ++u) {
+      const int32_t st = __builtin_amdgcn_readlane(cur.start, u);
+      const int32_t fr = __builtin_amdgcn_readlane(cur.freq, u);
       if (fr == IDF_FREQ_SCALE_ZERO && st == 0) {
-        flag |= IDF_STREAM_SCALE_ZERO;
-        stop = true;
+        stop = IDF_STREAM_SCALE_ZERO;
         break;
       }
-      uint64_t cdf = (uint64_t)(int64_t)st;  // vector<ull>.push_back(int)
-      uint64_t f = (uint64_t)(int64_t)fr;
-      if (state >= (f << 40)) {  // rans.pyx:62-64
-        out[nw++] = (uint32_t)(state & 0xffffffffull);
+      const uint64_t f = (uint64_t)(int64_t)fr;  // vector<ull>.push_back(int)
+      // rans.pyx:62-64: state >= f << 40; the low word of f << 40 is 0, so compare high words
+      if ((uint32_t)(state >> 32) >= ((uint32_t)fr << 8)) {
+        wbuf = lane == fill ? (uint32_t)state : wbuf;
+        if (++fill == 64) {
+          out[nw + lane] = wbuf;
+          nw += 64;
+          fill = 0;
+        }
         state >>= 32;
       }
       if (f == 0) {  // ZeroDivisionError, rans.cpp:1825-1834
-        flag |= IDF_STREAM_FREQ_ZERO;
-        stop = true;
+        stop = IDF_STREAM_FREQ_ZERO;
         break;
       }
+      const uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(mhi_v, u) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane(mlo_v, u);
       uint64_t q, r;
-      if (f <= (1ull << 24)) {
-        divmod_u64_u24(state, (uint32_t)f, rc_cur[u], q, r);
-      } else {  // only reachable out of window / corrupted input: exact slow path
-        q = state / f;
-        r = state % f;
+      if (fr > 0) {  // r < 2f < 2^32: the remainder and its correction in 32 bits
+        q = mulhi_u64(state, m);
+        uint32_t rr = (uint32_t)state - (uint32_t)q * (uint32_t)fr;
+        if (rr >= (uint32_t)fr) {
+          q += 1;
+          rr -= (uint32_t)fr;
+        }
+        r = rr;
+      } else {  // negative freq widened to a huge divisor (non-monotone CDF only)
+        divmod_u64_magic(state, f, m, q, r);
       }
-      state = (q << 24) + r + cdf;  // rans.pyx:65
-      flag |= cur[u].wflag;
+      state = (q << 24) + r + (uint64_t)(int64_t)st;  // rans.pyx:65
     }
-#pragma unroll
-    for (int u = 0; u < kEncAhead; ++u) {
-      cur[u] = nxt[u];
-      rc_cur[u] = rc_nxt[u];
-    }
+    if (lane < u) wflag |= cur.wflag;  // flags of the symbols coded
+    if (stop) break;
+    cur = nxt;
+    mcur = mnxt;
   }
-  final_state[k] = state;
-  nwords[k] = nw;
-  status[k] = flag;
+  if (lane < fill) out[nw + lane] = wbuf;
+  nw += fill;
+  // OR of the lanes' window flags
+  for (int d = 32; d >= 1; d >>= 1) wflag |= __shfl_xor(wflag, d, 64);
+  if (lane == 0) {
+    final_state[k] = state;
+    nwords[k] = nw;
+    status[k] = wflag | stop;
+  }
 }
 
 // ---------------------------------------------------------------- decode
@@ -560,7 +596,7 @@ int idf_rans_cdf_freq(void* stream, int64_t n, const float* x, const float* mean
 }
 
 int64_t idf_rans_encode_workspace_bytes(int64_t nsym) {
-  return (int64_t)(sizeof(EncSym) + sizeof(double)) * (nsym > 0 ? nsym : 1);
+  return (int64_t)(sizeof(EncSym) + sizeof(uint64_t)) * (nsym > 0 ? nsym : 1);
 }
 
 int idf_rans_encode_streams(void* stream, int64_t nstreams, int64_t nsym, const int64_t* sym_off,
@@ -572,14 +608,13 @@ int idf_rans_encode_streams(void* stream, int64_t nstreams, int64_t nsym, const 
   if (nstreams == 0) return IDF_OK;
   if (workspace_bytes < idf_rans_encode_workspace_bytes(nsym)) return IDF_ERR_WORKSPACE;
   EncSym* es = (EncSym*)workspace;
-  double* rcp = (double*)(es + (nsym > 0 ? nsym : 1));
+  uint64_t* rcp = (uint64_t*)(es + (nsym > 0 ? nsym : 1));
   int rc = IDF_OK;
   if (nsym > 0)
     hipLaunchKernelGGL(rans_encode_prep_kernel, dim3((unsigned)((nsym + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, nsym, x, mean, scale, es, rcp);
   if (rc) return rc;
-  int64_t blocks = (nstreams + 63) / 64;
-  hipLaunchKernelGGL(rans_encode_kernel, dim3((unsigned)blocks), dim3(64), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(rans_encode_kernel, dim3((unsigned)nstreams), dim3(64), 0, (hipStream_t)stream,
                      nstreams, sym_off, es, rcp, init_state, final_state, words, nwords, status);
   return idf_last_error();
 }
