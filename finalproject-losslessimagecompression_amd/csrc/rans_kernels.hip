@@ -190,40 +190,54 @@ __global__ void __launch_bounds__(64) rans_encode_kernel(
     for (; u < cnt; ++u) {
       const int32_t st = __builtin_amdgcn_readlane(cur.start, u);
       const int32_t fr = __builtin_amdgcn_readlane(cur.freq, u);
-      if (fr == IDF_FREQ_SCALE_ZERO && st == 0) {
-        stop = IDF_STREAM_SCALE_ZERO;
-        break;
-      }
-      const uint64_t f = (uint64_t)(int64_t)fr;  // vector<ull>.push_back(int)
-      // rans.pyx:62-64: state >= f << 40; the low word of f << 40 is 0, so compare high words
-      if ((uint32_t)(state >> 32) >= ((uint32_t)fr << 8)) {
-        wbuf = lane == fill ? (uint32_t)state : wbuf;
-        if (++fill == 64) {
-          out[nw + lane] = wbuf;
-          nw += 64;
-          fill = 0;
-        }
-        state >>= 32;
-      }
-      if (f == 0) {  // ZeroDivisionError, rans.cpp:1825-1834
-        stop = IDF_STREAM_FREQ_ZERO;
-        break;
-      }
       const uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(mhi_v, u) << 32) |
                          (uint32_t)__builtin_amdgcn_readlane(mlo_v, u);
-      uint64_t q, r;
-      if (fr > 0) {  // r < 2f < 2^32: the remainder and its correction in 32 bits
-        q = mulhi_u64(state, m);
-        uint32_t rr = (uint32_t)state - (uint32_t)q * (uint32_t)fr;
-        if (rr >= (uint32_t)fr) {
-          q += 1;
-          rr -= (uint32_t)fr;
+      if (fr <= 0) {  // rare: the scale-zero marker, a zero or a negative (non-monotone) freq
+        if (fr == IDF_FREQ_SCALE_ZERO && st == 0) {
+          stop = IDF_STREAM_SCALE_ZERO;
+          break;
         }
-        r = rr;
-      } else {  // negative freq widened to a huge divisor (non-monotone CDF only)
+        const uint64_t f = (uint64_t)(int64_t)fr;  // vector<ull>.push_back(int)
+        if (state >= (f << 40)) {                  // rans.pyx:62-64
+          wbuf = lane == fill ? (uint32_t)state : wbuf;
+          if (++fill == 64) {
+            out[nw + lane] = wbuf;
+            nw += 64;
+            fill = 0;
+          }
+          state >>= 32;
+        }
+        if (f == 0) {  // ZeroDivisionError, rans.cpp:1825-1834
+          stop = IDF_STREAM_FREQ_ZERO;
+          break;
+        }
+        uint64_t q, r;
         divmod_u64_magic(state, f, m, q, r);
+        state = (q << 24) + r + (uint64_t)(int64_t)st;  // rans.pyx:65
+        continue;
       }
-      state = (q << 24) + r + (uint64_t)(int64_t)st;  // rans.pyx:65
+      // rans.pyx:62-64: state >= f << 40; the low word of f << 40 is 0, so compare high
+      // words.  Branch-free: the word goes to lane `fill` only when emitted.
+      const uint32_t sh = (uint32_t)(state >> 32);
+      const bool emit = sh >= ((uint32_t)fr << 8);
+      wbuf = lane == (emit ? fill : 64) ? (uint32_t)state : wbuf;
+      fill += emit ? 1 : 0;
+      state = emit ? (uint64_t)sh : state;
+      if (fill == 64) {
+        out[nw + lane] = wbuf;
+        nw += 64;
+        fill = 0;
+      }
+      // rans.pyx:65 with q = state / f from the magic reciprocal (q or q - 1); the
+      uint64_t q = mulhi_u64(state, m);
+      // remainder and its correction fit 32 bits; rr - f borrows (bit 31) iff rr < f
+      const uint32_t rr = (uint32_t)state - (uint32_t)q * (uint32_t)fr;
+      const uint32_t d = rr - (uint32_t)fr;
+      uint32_t borrow = d >> 31;
+      asm("" : "+s"(borrow));  // opaque: a scalar shift, not a compare + VALU bool select
+      q += 1u - borrow;
+      const uint32_t r = d < rr ? d : rr;
+      state = (q << 24) + r + (uint64_t)(int64_t)st;
     }
     if (lane < u) wflag |= cur.wflag;  // flags of the symbols coded
     if (stop) break;
