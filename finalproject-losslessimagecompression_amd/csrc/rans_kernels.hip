@@ -395,19 +395,26 @@ __device__ __forceinline__ bool exact_window(uint64_t mod, int lower, float mi, 
   return true;
 }
 
-__global__ void __launch_bounds__(64) rans_decode_kernel(
+// WAVES streams per block, one per wave: the waves never synchronise after the table
+// load, so packing them only concentrates the decode on fewer CUs (nstreams / WAVES), which
+// leaves the rest of the chip to a concurrent lane's convolutions (ImageCodec lanes).
+template <int WAVES>
+__global__ void __launch_bounds__(64 * WAVES) rans_decode_kernel(
     int64_t nstreams, const int64_t* __restrict__ sym_off, const int64_t* __restrict__ word_off,
     const int64_t* __restrict__ nwords, const uint32_t* __restrict__ words,
     const float* __restrict__ mean, const float* __restrict__ scale,
     const uint64_t* __restrict__ init_state, uint64_t* __restrict__ final_state,
     float* __restrict__ out, int32_t* __restrict__ status, const int32_t* __restrict__ btab) {
   __shared__ uint64_t tab[32];
-  __shared__ __attribute__((aligned(16))) int32_t bt[2][64 * 64];  // block estimates, 2 windows
+  // block estimates, 2 windows per wave
+  __shared__ __attribute__((aligned(16))) int32_t bt_all[WAVES][2][64 * 64];
   if (threadIdx.x < 32) tab[threadIdx.x] = kExp2fTab[threadIdx.x];
   __syncthreads();
-  const int64_t k = blockIdx.x;
+  const int wave = WAVES == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t k = (int64_t)blockIdx.x * WAVES + wave;
   if (k >= nstreams) return;
-  const int lane = threadIdx.x;
+  auto& bt = bt_all[wave];
+  const int lane = threadIdx.x & 63;
   const int64_t b = sym_off[k], n = sym_off[k + 1] - b;
   const uint32_t* w = words + word_off[k];
   int64_t pos = nwords[k];
@@ -633,6 +640,13 @@ int idf_rans_encode_streams(void* stream, int64_t nstreams, int64_t nsym, const 
   return idf_last_error();
 }
 
+// IDF_DECODE_WPB=4: four streams per block (a quarter of the CUs; measured 1-2% slower alone,
+// the waves share the CU's scalar unit); default one stream per block.
+static int decode_waves_per_block() {
+  const char* e = getenv("IDF_DECODE_WPB");
+  return (e && atoi(e) == 4) ? 4 : 1;
+}
+
 int64_t idf_rans_decode_workspace_bytes(int64_t nsym) {
   return 64 * (int64_t)sizeof(int32_t) * (nsym > 0 ? nsym : 1);
 }
@@ -649,9 +663,14 @@ int idf_rans_decode_streams(void* stream, int64_t nstreams, int64_t nsym, const 
   if (nsym > 0)
     hipLaunchKernelGGL(rans_decode_prep_kernel, dim3((unsigned)((nsym * 64 + 255) / 256)), dim3(256),
                        0, (hipStream_t)stream, nsym, mean, scale, btab);
-  hipLaunchKernelGGL(rans_decode_kernel, dim3((unsigned)nstreams), dim3(64), 0,
-                     (hipStream_t)stream, nstreams, sym_off, word_off, nwords, words, mean, scale,
-                     init_state, final_state, out, status, btab);
+  if (decode_waves_per_block() == 4)
+    hipLaunchKernelGGL(rans_decode_kernel<4>, dim3((unsigned)((nstreams + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, nstreams, sym_off, word_off, nwords, words, mean,
+                       scale, init_state, final_state, out, status, btab);
+  else
+    hipLaunchKernelGGL(rans_decode_kernel<1>, dim3((unsigned)nstreams), dim3(64), 0,
+                       (hipStream_t)stream, nstreams, sym_off, word_off, nwords, words, mean,
+                       scale, init_state, final_state, out, status, btab);
   return idf_last_error();
 }
 

@@ -13,6 +13,7 @@ that slice would, and is bit-identical to it.
 """
 from __future__ import annotations
 
+import os
 import struct
 from dataclasses import dataclass, field
 
@@ -107,7 +108,7 @@ class StreamCoder:
         self.engine = engine
         self._off = {}
         self._lvl = {}
-        self._dws = None
+        self._dws = {}  # decode scratch per workspace slot (lanes decode concurrently)
 
     def sym_off(self, B: int) -> torch.Tensor:
         t = self._off.get(B)
@@ -167,27 +168,47 @@ class StreamCoder:
             self._lvl[key] = hit
         return hit
 
-    def decode_level(self, bs: Bitstream, B: int, l: int, ws, word_off, out_state, out_status):
+    def decode_level(self, bs: Bitstream, B: int, l: int, ws, word_off, out_state, out_status,
+                     img0: int = 0, n_img: int | None = None, slot: int = 0):
+        """Decodes level l of images [img0, img0 + n_img) of the B-image bitstream bs into
+        ws (a workspace laid out for n_img images)."""
         eng = self.engine
         s = _lib.stream_ptr(eng.device)
-        base, nsym, rel = self.level_streams(B, l)
-        k0 = l * B
+        nb = B if n_img is None else n_img
+        base, nsym, rel = self.level_streams(nb, l)
+        k0 = l * B + img0
         wbytes = lib().idf_rans_decode_workspace_bytes(nsym)
-        if self._dws is None or self._dws.numel() < wbytes:
-            self._dws = torch.empty(wbytes, dtype=torch.uint8, device=eng.device)
+        dws = self._dws.get(slot)
+        if dws is None or dws.numel() < wbytes:
+            dws = self._dws[slot] = torch.empty(wbytes, dtype=torch.uint8, device=eng.device)
         check(lib().idf_rans_decode_streams(
-            s, B, nsym, ptr(rel), ptr(word_off) + 8 * k0, ptr(bs.nwords) + 8 * k0, ptr(bs.words),
+            s, nb, nsym, ptr(rel), ptr(word_off) + 8 * k0, ptr(bs.nwords) + 8 * k0, ptr(bs.words),
             ptr(ws["mean"]) + 4 * base, ptr(ws["scale"]) + 4 * base, ptr(bs.states) + 8 * k0,
             ptr(out_state) + 8 * k0, ptr(ws["lat"]) + 4 * base, ptr(out_status) + 4 * k0,
-            ptr(self._dws), wbytes), "rans decode")
+            ptr(dws), wbytes), "rans decode")
 
 
 class ImageCodec:
-    """uint8 NCHW images <-> Bitstream with a FlowEngine (IDFlows configs)."""
+    """uint8 NCHW images <-> Bitstream with a FlowEngine (IDFlows configs).
 
-    def __init__(self, engine):
+    Decode lanes (opt-in, IDF_LANES / `lanes`; default 1): a batch of B >= 2 * LANE_MIN
+    images decodes as `lanes` equal sub-batches, each on its own HIP stream and workspace
+    slot, lane i+1 waiting for lane i's top-level decode.  The aim was to run one lane's
+    serial rANS decode (a few CUs for milliseconds) beside another lane's flow convs.
+    Measured on MI355X: no gain -- the second lane's queue is not serviced
+    until the first lane is deep into its last level, with an event or a host-side stagger,
+    separate high-priority decode streams, 1 or 4 decode waves per block.  Kept because it
+    is exact (the convs are batch-invariant, so every stream decodes identically to the
+    single-lane decode: tests/test_gpu_lanes.py) and is the hook for a CU-partitioned
+    schedule."""
+
+    LANE_MIN = 8
+
+    def __init__(self, engine, lanes: int | None = None):
         self.engine = engine
         self.coder = StreamCoder(engine)
+        self.lanes = int(os.environ.get("IDF_LANES", "1")) if lanes is None else int(lanes)
+        self._streams = []
 
     @torch.no_grad()
     def encode(self, img_u8: torch.Tensor, cond=None, compact: bool = True) -> Bitstream:
@@ -233,17 +254,29 @@ class ImageCodec:
     @torch.no_grad()
     def decode_nchw(self, bs: Bitstream, cond=None, verify: bool = True):
         """inverse of encode_nchw -> (float NCHW, info)."""
-        ws, info = self._decode_ws(bs, cond)
-        x = self.engine.image_nchw(ws, bs.n_images)
+        eng = self.engine
+        x = torch.empty((bs.n_images, eng.C, eng.H, eng.W), dtype=torch.float32,
+                        device=eng.device)
+        info = self._decode_lanes(bs, cond,
+                                  lambda i, b0, n, ws: eng.image_nchw(ws, n, out=x[b0:b0 + n]))
         if verify:
             info["ok"] = bool((info["final_states"] == RANS_L).all().item()) and not bool(
                 (info["status"] & ~_lib.STREAM_WORDS_LEFT).any().item())
         return x, info
 
-    def _decode_ws(self, bs: Bitstream, cond):
-        eng = self.engine
-        dev = eng.device
-        B = bs.n_images
+    def _n_lanes(self, B: int) -> int:
+        n = max(1, self.lanes)
+        while n > 1 and (B % n or B // n < self.LANE_MIN):
+            n -= 1
+        return n
+
+    def _lane_streams(self, n: int):
+        while len(self._streams) < n:
+            self._streams.append(torch.cuda.Stream(self.engine.device))
+        return self._streams[:n]
+
+    def _prep_decode(self, bs: Bitstream):
+        dev = self.engine.device
         if bs.states.device != dev:
             bs = Bitstream(bs.n_images, bs.level_shapes, bs.states.to(dev), bs.nwords.to(dev),
                            bs.words.to(dev), None, bs.meta)
@@ -254,25 +287,61 @@ class ImageCodec:
             bs.words = torch.zeros(1, dtype=torch.int32, device=dev)
         out_state = torch.empty_like(bs.states)
         out_status = torch.zeros(bs.n_streams, dtype=torch.int32, device=dev)
+        return bs, word_off, out_state, out_status
 
-        def dec(l, ws):
-            self.coder.decode_level(bs, B, l, ws, word_off, out_state, out_status)
-
+    def _decode_lanes(self, bs: Bitstream, cond, finish):
+        """Runs the top-down decode of bs in lanes; finish(i, img0, n, ws) is issued on lane
+        i's stream after its flows.  Returns the decode info."""
+        eng = self.engine
+        B = bs.n_images
+        bs, word_off, out_state, out_status = self._prep_decode(bs)
+        nl = self._n_lanes(B)
+        h = B // nl
         # the convs must run as the encoder ran them (bit-identical couplings)
         mode, prev = bs.meta.get("conv", "f32"), eng.conv_mode
         if mode != prev:
             eng.set_conv_mode(mode)
         try:
-            ws = eng.inverse_pm(B, dec, cond=cond)
+            if nl == 1:
+                def dec(l, ws):
+                    self.coder.decode_level(bs, B, l, ws, word_off, out_state, out_status)
+                ws = eng.inverse_pm(B, dec, cond=cond)
+                finish(0, 0, B, ws)
+            else:
+                main = torch.cuda.current_stream(eng.device)
+                eng.ensure_top_prior(eng.workspace(h, 0), _lib.stream_ptr(eng.device))
+                go = torch.cuda.Event()
+                go.record(main)
+                top = eng.nsplit - 1
+                for i, st in enumerate(self._lane_streams(nl)):
+                    st.wait_event(go)
+                    staggered = torch.cuda.Event()
+
+                    def dec(l, ws, i=i, st=st, ev=staggered):
+                        self.coder.decode_level(bs, B, l, ws, word_off, out_state, out_status,
+                                                img0=i * h, n_img=h, slot=i)
+                        if l == top:
+                            ev.record(st)
+                    with torch.cuda.stream(st):
+                        ci = None if cond is None else cond[i * h:(i + 1) * h].contiguous()
+                        ws = eng.inverse_pm(h, dec, cond=ci, slot=i)
+                        finish(i, i * h, h, ws)
+                    go = staggered
+                for st in self._lane_streams(nl):
+                    main.wait_stream(st)
         finally:
             if mode != prev:
                 eng.set_conv_mode(prev)
-        return ws, {"final_states": out_state, "status": out_status}
+        return {"final_states": out_state, "status": out_status}
 
     @torch.no_grad()
     def decode(self, bs: Bitstream, cond=None, verify: bool = True):
-        ws, info = self._decode_ws(bs, cond)
-        img, bad = self.engine.image_u8(ws, bs.n_images)
+        eng = self.engine
+        img = torch.empty((bs.n_images, eng.C, eng.H, eng.W), dtype=torch.uint8,
+                          device=eng.device)
+        bad = torch.zeros(1, dtype=torch.int32, device=eng.device)
+        info = self._decode_lanes(
+            bs, cond, lambda i, b0, n, ws: eng.image_u8(ws, n, out=img[b0:b0 + n], bad=bad))
         info["off_grid"] = bad
         if verify:
             ok = bool((info["final_states"] == RANS_L).all().item()) and int(bad.item()) == 0

@@ -294,8 +294,10 @@ class FlowEngine:
         return {"couple": c, "prior": p, "total": c + p}
 
     # ------------------------------------------------------------ workspace
-    def workspace(self, B: int):
-        ws = self._ws.get(B)
+    def workspace(self, B: int, slot: int = 0):
+        """Activation / latent buffers for B images.  Each slot is an independent set (the
+        ImageCodec lanes run one slot per HIP stream); one batch size stays resident."""
+        ws = self._ws.get((B, slot))
         if ws is not None:
             return ws
         dev = self.device
@@ -316,7 +318,8 @@ class FlowEngine:
             ws["cond"] = [f(B * L.h * L.w * round_up(L.cond_ch, 4)) for L in self.levels]
             # channels C..3 of the 4-wide pixel rows stay zero (they meet zero weights)
             ws["cond_img"] = torch.zeros(B * self.H * self.W * 4, dtype=torch.float32, device=dev)
-        self._ws = {B: ws}  # keep one batch size resident
+        self._ws = {k: v for k, v in self._ws.items() if k[0] == B}  # one batch size resident
+        self._ws[(B, slot)] = ws
         return ws
 
     # ------------------------------------------------------------ pieces
@@ -372,6 +375,13 @@ class FlowEngine:
         blk.run(s, B, Lv.h, Lv.w, ptr(feat), ld, ptr(ws["tmp"]), self.ld_tmp,
                 head_prior(Lv.z, mean, logscale, scale))
 
+    def ensure_top_prior(self, ws, s):
+        """Computes the cached top prior on stream s if it is needed and missing (the lanes
+        call this on their parent stream before forking, so no lane races its creation)."""
+        Lv = self.levels[-1]
+        if self._top_prior is None and Lv.prior_x_zero and not self.conditional:
+            self._top_prior_cached(ws, 0, s, 0)
+
     def _top_prior_cached(self, ws, B, s, off):
         """IDFlows' top prior sees zeros (priorlib.py:43): its output does not depend on
         the data, so it is computed once (batch 1) and replicated per image."""
@@ -388,11 +398,11 @@ class FlowEngine:
 
     # ------------------------------------------------------------ forward
     @torch.no_grad()
-    def forward_pm(self, B: int, cond=None):
+    def forward_pm(self, B: int, cond=None, slot: int = 0):
         """Runs flows.py:87-116 from ws['img'] (pixel-major, ld 4) for B images.
         Fills ws lat/mean/logscale/scale.  Returns the workspace."""
         L = lib()
-        ws = self.workspace(B)
+        ws = self.workspace(B, slot)
         s = _lib.stream_ptr(self.device)
         offs = self.sym_offsets(B)
         if self.conditional:
@@ -429,16 +439,16 @@ class FlowEngine:
             src, ld_src, H, W, C = ptr(x) + Lv.z * FLOAT, Lv.ldx, Lv.h, Lv.w, Lv.rest
         return ws
 
-    def load_u8(self, img_u8: torch.Tensor):
+    def load_u8(self, img_u8: torch.Tensor, slot: int = 0):
         B = img_u8.shape[0]
-        ws = self.workspace(B)
+        ws = self.workspace(B, slot)
         check(lib().idf_dequant_u8(_lib.stream_ptr(self.device), B, self.C, self.H, self.W,
                                    ptr(img_u8), ptr(ws["img"]), 4), "dequant")
         return ws
 
-    def load_nchw(self, x: torch.Tensor):
+    def load_nchw(self, x: torch.Tensor, slot: int = 0):
         B = x.shape[0]
-        ws = self.workspace(B)
+        ws = self.workspace(B, slot)
         x = x.contiguous().float()
         check(lib().idf_nchw_to_pm(_lib.stream_ptr(self.device), B, self.C, self.H, self.W, ptr(x),
                                    ptr(ws["img"]), 4), "nchw_to_pm")
@@ -446,12 +456,12 @@ class FlowEngine:
 
     # ------------------------------------------------------------ inverse
     @torch.no_grad()
-    def inverse_pm(self, B: int, decode_level, cond=None, priors: bool = True):
+    def inverse_pm(self, B: int, decode_level, cond=None, priors: bool = True, slot: int = 0):
         """Top-down decoder (flows.py:118-152 order).  For each level l (top first):
         prior -> decode_level(l, ws) fills ws['lat'] level l -> flows backward ->
         unsqueeze.  The image lands in ws['img'] (pixel-major, ld 4)."""
         L = lib()
-        ws = self.workspace(B)
+        ws = self.workspace(B, slot)
         s = _lib.stream_ptr(self.device)
         offs = self.sym_offsets(B)
         if self.conditional and priors:
@@ -496,15 +506,20 @@ class FlowEngine:
                   "unsqueeze")
         return ws
 
-    def image_nchw(self, ws, B):
-        out = torch.empty((B, self.C, self.H, self.W), dtype=torch.float32, device=self.device)
+    def image_nchw(self, ws, B, out=None):
+        if out is None:
+            out = torch.empty((B, self.C, self.H, self.W), dtype=torch.float32, device=self.device)
         check(lib().idf_pm_to_nchw(_lib.stream_ptr(self.device), B, self.C, self.H, self.W,
                                    ptr(ws["img"]), 4, ptr(out)), "pm_to_nchw")
         return out
 
-    def image_u8(self, ws, B):
-        out = torch.empty((B, self.C, self.H, self.W), dtype=torch.uint8, device=self.device)
-        bad = torch.zeros(1, dtype=torch.int32, device=self.device)
+    def image_u8(self, ws, B, out=None, bad=None):
+        """ws['img'] -> uint8 NCHW (out: a contiguous [B, C, H, W] view to fill) and the
+        off-grid pixel count (added into bad)."""
+        if out is None:
+            out = torch.empty((B, self.C, self.H, self.W), dtype=torch.uint8, device=self.device)
+        if bad is None:
+            bad = torch.zeros(1, dtype=torch.int32, device=self.device)
         check(lib().idf_quant_u8(_lib.stream_ptr(self.device), B, self.C, self.H, self.W,
                                  ptr(ws["img"]), 4, ptr(out), ptr(bad)), "quant")
         return out, bad
