@@ -237,7 +237,7 @@ def main():
     _lib.lib().idf_timer_destroy(timer)
 
     flops = eng.flops_per_image()["total"]
-    kname = ("conv3_wino_kernel<3, 448, true, false>" if eng.conv_mode == "x3"
+    kname = ("conv3_wino_kernel<3, 448, true, false," if eng.conv_mode == "x3"
              else "conv3_wino_kernel<3, 448, false")
     traffic, traffic_src = pmc_traffic(kname) if eng.wino else (None, None)
     # the x3 kernel's products run on f16 MFMA: price them against the f16 dense peak
