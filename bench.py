@@ -30,6 +30,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 PEAK_F32_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 matrix (f32-in MFMA) = vector peak
+PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E
 PEAK_F16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 dense MFMA peak
 B_PER_GPU = 256
 PX_PER_IMG = 64 * 64
@@ -70,6 +71,35 @@ def pmc_traffic(kernel: str):
     if f is None or w is None:
         return None, None
     return (2.0 * f + w) * 1024.0, os.path.relpath(d, REPO)
+
+
+def rans_roofline(trace, bs, steps):
+    """rANS encode / decode (prep + serial pass per launch pair), timed with HIP events on
+    the launch stream over the timed steps, against the HBM roofline.  Algorithmic bytes:
+    encode reads x, mean, scale (12 B/symbol) and writes the words (4 B each) plus a state
+    and a word count per stream (16 B); decode reads mean, scale (8 B/symbol), the words and
+    the states and writes x (4 B/symbol) plus a final state per stream.  The serial chains
+    (one rANS state per stream, rans.pyx's reference order) make both latency-bound:
+    ns_per_symbol is the chain's time per symbol (launch time / symbols per stream)."""
+    out = {}
+    words = bs.total_words()
+    for kind in ("encode", "decode"):
+        recs = [r for r in trace if r[0] == kind]
+        if not recs:
+            continue
+        ms = sum(a.elapsed_time(b) for _, _, _, a, b in recs)
+        nsym = sum(r[1] for r in recs)
+        chain = sum(r[1] / max(r[2], 1) for r in recs)
+        nstr = sum(r[2] for r in recs)
+        byts = 12.0 * nsym + 4.0 * words * steps + 16.0 * nstr
+        gbs = byts / (ms * 1e-3) / 1e9
+        out[kind] = {"ms_per_step": round(ms / steps, 4),
+                     "msym_s": round(nsym / (ms * 1e-3) / 1e6, 2),
+                     "ns_per_symbol": round(ms * 1e6 / chain, 1),
+                     "bound": "latency (serial state chain per stream)",
+                     "achieved": round(gbs, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(gbs / PEAK_HBM_GBS, 5)}
+    return out
 
 
 def conv_kernel_name(eng):
@@ -201,6 +231,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    codec.coder.trace = []  # HIP events around the rANS launches of the timed steps
     t0 = time.perf_counter()
     evs = []
     for _ in range(args.steps):
@@ -215,6 +246,8 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    rans = rans_roofline(codec.coder.trace, bs, args.steps)
+    codec.coder.trace = None
     enc_ms = sum(a.elapsed_time(b) for a, b, _ in evs) / len(evs)
     dec_ms = sum(b.elapsed_time(c) for _, b, c in evs) / len(evs)
 
@@ -300,6 +333,7 @@ def main():
                 "conv1x1_achieved": round(c1_tflops, 3),
                 "conv1x1_avg_launch_ms": round(c1_avg_ms, 5),
             },
+            "rans": rans,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)

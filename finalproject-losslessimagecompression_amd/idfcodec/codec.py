@@ -109,6 +109,16 @@ class StreamCoder:
         self._off = {}
         self._lvl = {}
         self._dws = {}  # decode scratch per workspace slot (lanes decode concurrently)
+        # when a list: (kind, n_symbols, n_streams, start, end) timing events around every
+        # rANS launch pair (prep + serial pass) on the launch stream (bench.py)
+        self.trace = None
+
+    def _mark(self):
+        if self.trace is None:
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
 
     def sym_off(self, B: int) -> torch.Tensor:
         t = self._off.get(B)
@@ -138,10 +148,13 @@ class StreamCoder:
         wsp = ws.get("rans_ws")
         if wsp is None or wsp.numel() < wbytes:
             wsp = ws["rans_ws"] = torch.empty(wbytes, dtype=torch.uint8, device=dev)
+        e0 = self._mark()
         check(lib().idf_rans_encode_streams(s, ns, nsym, ptr(off), ptr(ws["lat"]), ptr(ws["mean"]),
                                             ptr(ws["scale"]), ptr(init), ptr(final), ptr(scratch),
                                             ptr(nwords), ptr(status), ptr(wsp), wbytes),
               "rans encode")
+        if e0 is not None:
+            self.trace.append(("encode", nsym, ns, e0, self._mark()))
         shapes = [(L.z, L.h, L.w) for L in eng.levels]
         meta = {"n_subpixels": B * eng.C * eng.H * eng.W}
         if not compact:
@@ -181,11 +194,14 @@ class StreamCoder:
         dws = self._dws.get(slot)
         if dws is None or dws.numel() < wbytes:
             dws = self._dws[slot] = torch.empty(wbytes, dtype=torch.uint8, device=eng.device)
+        e0 = self._mark()
         check(lib().idf_rans_decode_streams(
             s, nb, nsym, ptr(rel), ptr(word_off) + 8 * k0, ptr(bs.nwords) + 8 * k0, ptr(bs.words),
             ptr(ws["mean"]) + 4 * base, ptr(ws["scale"]) + 4 * base, ptr(bs.states) + 8 * k0,
             ptr(out_state) + 8 * k0, ptr(ws["lat"]) + 4 * base, ptr(out_status) + 4 * k0,
             ptr(dws), wbytes), "rans decode")
+        if e0 is not None:
+            self.trace.append(("decode", nsym, nb, e0, self._mark()))
 
 
 class ImageCodec:
