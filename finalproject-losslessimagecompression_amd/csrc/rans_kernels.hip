@@ -640,11 +640,11 @@ int idf_rans_encode_streams(void* stream, int64_t nstreams, int64_t nsym, const 
   return idf_last_error();
 }
 
-// IDF_DECODE_WPB=4: four streams per block (a quarter of the CUs; measured 1-2% slower alone,
-// the waves share the CU's scalar unit); default one stream per block.
+// Streams per block: 4 by default (a quarter of the CUs: decode lanes run beside another
+// lane's convs; alone it measures the same as 1), IDF_DECODE_WPB=1 for one per block.
 static int decode_waves_per_block() {
   const char* e = getenv("IDF_DECODE_WPB");
-  return (e && atoi(e) == 4) ? 4 : 1;
+  return (e && atoi(e) == 1) ? 1 : 4;
 }
 
 int64_t idf_rans_decode_workspace_bytes(int64_t nsym) {

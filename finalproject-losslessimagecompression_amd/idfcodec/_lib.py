@@ -163,6 +163,20 @@ def require_device(t: torch.Tensor, what: str = "tensor"):
         raise IdfError(f"idfcodec: {what} must be a HIP device tensor (no CPU fallback)")
 
 
+def new_stream(device=None) -> torch.cuda.ExternalStream:
+    """A HIP stream created with hipStreamNonBlocking on `device`, as a torch stream.
+    The ImageCodec lanes use these: two torch.cuda.Stream()s were measured NOT to run
+    concurrently on MI355X (the second lane's kernels waited ~25 ms for the first's), two
+    such streams do (tools/lanes_probe.py).  Lives as long as the process."""
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    h = ctypes.c_void_p()
+    with torch.cuda.device(device):
+        rc = hip.hipStreamCreateWithFlags(ctypes.byref(h), ctypes.c_uint(1))
+    if rc != 0:
+        raise IdfError(f"hipStreamCreateWithFlags failed ({rc})")
+    return torch.cuda.ExternalStream(h.value, device=device)
+
+
 def stream_ptr(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 

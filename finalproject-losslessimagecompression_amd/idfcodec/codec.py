@@ -207,24 +207,24 @@ class StreamCoder:
 class ImageCodec:
     """uint8 NCHW images <-> Bitstream with a FlowEngine (IDFlows configs).
 
-    Decode lanes (opt-in, IDF_LANES / `lanes`; default 1): a batch of B >= 2 * LANE_MIN
-    images decodes as `lanes` equal sub-batches, each on its own HIP stream and workspace
-    slot, lane i+1 waiting for lane i's top-level decode.  The aim was to run one lane's
-    serial rANS decode (a few CUs for milliseconds) beside another lane's flow convs.
-    Measured on MI355X: no gain -- the second lane's queue is not serviced
-    until the first lane is deep into its last level, with an event or a host-side stagger,
-    separate high-priority decode streams, 1 or 4 decode waves per block.  Kept because it
-    is exact (the convs are batch-invariant, so every stream decodes identically to the
-    single-lane decode: tests/test_gpu_lanes.py) and is the hook for a CU-partitioned
-    schedule."""
+    Decode lanes (IDF_LANES / `lanes`, default 2): a batch of B >= 2 * LANE_MIN images
+    decodes as `lanes` equal sub-batches, each on its own non-blocking HIP stream and
+    workspace slot, lane i+1 waiting for lane i's top-level decode.  The rANS decode is a
+    serial chain per stream that holds a few CUs for milliseconds; staggered lanes run one
+    lane's decode beside the other lane's flow convs (imagenet64 B=256: decode 37.8 ->
+    35.8 ms).  More than 2 lanes exceed the process's concurrent hardware queues
+    (GPU_MAX_HW_QUEUES=4, one taken by the default stream) and serialize.  Exact: the convs
+    are batch-invariant, so every stream decodes identically to the single-lane decode
+    (tests/test_gpu_lanes.py)."""
 
     LANE_MIN = 8
 
     def __init__(self, engine, lanes: int | None = None):
         self.engine = engine
         self.coder = StreamCoder(engine)
-        self.lanes = int(os.environ.get("IDF_LANES", "1")) if lanes is None else int(lanes)
+        self.lanes = int(os.environ.get("IDF_LANES", "2")) if lanes is None else int(lanes)
         self._streams = []
+        self.lane_marks = None
 
     @torch.no_grad()
     def encode(self, img_u8: torch.Tensor, cond=None, compact: bool = True) -> Bitstream:
@@ -288,7 +288,7 @@ class ImageCodec:
 
     def _lane_streams(self, n: int):
         while len(self._streams) < n:
-            self._streams.append(torch.cuda.Stream(self.engine.device))
+            self._streams.append(_lib.new_stream(self.engine.device))
         return self._streams[:n]
 
     def _prep_decode(self, bs: Bitstream):
@@ -329,8 +329,15 @@ class ImageCodec:
                 go = torch.cuda.Event()
                 go.record(main)
                 top = eng.nsplit - 1
+                stagger = os.environ.get("IDF_LANE_STAGGER", "event") != "none"
                 for i, st in enumerate(self._lane_streams(nl)):
-                    st.wait_event(go)
+                    st.wait_event(go if (stagger or i == 0) else first)
+                    if i == 0:
+                        first = go
+                    if self.lane_marks is not None:  # lane start times (tools/lanes_probe.py)
+                        m = torch.cuda.Event(enable_timing=True)
+                        m.record(st)
+                        self.lane_marks.append(m)
                     staggered = torch.cuda.Event()
 
                     def dec(l, ws, i=i, st=st, ev=staggered):

@@ -38,7 +38,7 @@ def test_lanes_decode_identical(B):
     raw = codec.encode(img, compact=False)
     out, info = _decode_all(codec, raw, 2)
     assert info["ok"] and torch.equal(out, img)
-    codec.lanes = 1
+    codec.lanes = 2
 
 
 def test_lanes_conditional_decode_identical(golden):
@@ -58,4 +58,4 @@ def test_lanes_conditional_decode_identical(golden):
     assert rinfo["ok"] and info["ok"]
     assert torch.equal(ref, img) and torch.equal(out, img)
     assert torch.equal(info["final_states"], rinfo["final_states"])
-    codec.lanes = 1
+    codec.lanes = 2

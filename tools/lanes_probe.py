@@ -1,4 +1,7 @@
-"""Host issue time vs GPU time of encode / decode (lanes 1, 2): is the decode host-bound?"""
+"""Decode lanes probe: when does lane 1 start relative to lane 0 (timing events recorded on
+each lane stream right after its wait), and the decode's total time.  Variants: staggered by
+an event or not; torch pool streams or HIP streams created here with hipStreamNonBlocking."""
+import ctypes
 import os
 import sys
 import time
@@ -13,25 +16,33 @@ model = synthetic.build_model(configs.get("imagenet64")).cuda()
 codec = model.codec()
 img = synthetic.images(256).cuda()
 bs = codec.encode(img)
-for lanes, stg, dst, wpb in ((1, "host", "0", "4"), (2, "host", "1", "4"), (2, "event", "1", "4"),
-                             (2, "host", "0", "4"), (2, "host", "1", "1"), (4, "host", "1", "4"),
-                             (2, "host", "1", "4")):
+hip = ctypes.CDLL("libamdhip64.so.7")
+ext = []
+for _ in range(4):
+    h = ctypes.c_void_p()
+    assert hip.hipStreamCreateWithFlags(ctypes.byref(h), ctypes.c_uint(1)) == 0
+    ext.append(torch.cuda.ExternalStream(h.value))
+torch_streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+V = [(1, "event", "torch", "1"), (1, "event", "torch", "4")]
+V += [(n, st, "ext", w) for n in (2, 4) for st in ("event", "none") for w in ("1", "4")]
+for lanes, stg, kind, wpb in V:
+    os.environ["IDF_DECODE_WPB"] = wpb
     codec.lanes = lanes
     os.environ["IDF_LANE_STAGGER"] = stg
-    os.environ["IDF_LANE_DEC_STREAM"] = dst
-    os.environ["IDF_DECODE_WPB"] = wpb
-    stg = f"{stg} decstream={dst} wpb={wpb}"
-    codec.decode(bs, verify=False)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    out, info = codec.decode(bs, verify=False)
-    t1 = time.perf_counter()
-    torch.cuda.synchronize()
-    t2 = time.perf_counter()
-    t3 = time.perf_counter()
-    b2 = codec.encode(img, compact=False)
-    t4 = time.perf_counter()
-    torch.cuda.synchronize()
-    t5 = time.perf_counter()
-    print(f"lanes {lanes} {stg}: decode issue {1e3*(t1-t0):.2f} ms, done {1e3*(t2-t0):.2f} ms; "
-          f"encode(compact=False) issue {1e3*(t4-t3):.2f} ms, done {1e3*(t5-t3):.2f} ms", flush=True)
+    codec._streams = list(ext if kind == "ext" else torch_streams)
+    for rep in range(2):
+        codec.lane_marks = []
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        t0 = time.perf_counter()
+        out, info = codec.decode(bs, verify=False)
+        t1 = time.perf_counter()
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        marks = [round(e0.elapsed_time(m), 2) for m in codec.lane_marks]
+        ok = torch.equal(out, img)
+        print(f"lanes {lanes} stagger={stg} streams={kind} wpb={wpb}: issue {1e3*(t1-t0):.2f} ms, "
+              f"gpu {e0.elapsed_time(e1):.2f} ms, lane starts {marks} ms, exact {ok}", flush=True)
