@@ -1,5 +1,8 @@
-# ad-hoc GPU step (edited per experiment): rANS encode timings + rANS/codec parity + bench
+# ad-hoc GPU step (edited per experiment): bench lanes 1 vs 2, more steps
 set -o pipefail
 mkdir -p gpurun_out
-cd tools/native && timeout -k 10 60 ./rans_bench_v1 6144 > ../../gpurun_out/rb_v1.log 2>&1 && timeout -k 10 60 ./rans_bench_0 6144 > ../../gpurun_out/rb_new.log 2>&1 && cd ../.. && cat gpurun_out/rb_v1.log gpurun_out/rb_new.log && \
-timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_rans.py tests/test_gpu_codec.py > gpurun_out/t_rans.log 2>&1; rc=$?; tail -3 gpurun_out/t_rans.log; [ $rc -eq 0 ] && timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench_enc.log 2>&1 && tail -1 gpurun_out/bench_enc.log | cut -c1-600
+export PYTHONDONTWRITEBYTECODE=1
+for v in "IDF_LANES=1" "IDF_LANES=2" "IDF_LANES=1" "IDF_LANES=2"; do
+  env $v timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/b.log 2>&1 || exit $?
+  echo "$v: $(tail -1 gpurun_out/b.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["encode_ms"], d["decode_ms"], d["round_trip_exact"])')"
+done
