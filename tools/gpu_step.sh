@@ -1,8 +1,11 @@
-# ad-hoc GPU step (edited per experiment): bench lanes 1 vs 2, more steps
+# ad-hoc GPU step (edited per experiment): residual configs with decode lanes 1 vs 2
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONDONTWRITEBYTECODE=1
-for v in "IDF_LANES=1" "IDF_LANES=2" "IDF_LANES=1" "IDF_LANES=2"; do
-  env $v timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/b.log 2>&1 || exit $?
-  echo "$v: $(tail -1 gpurun_out/b.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["encode_ms"], d["decode_ms"], d["round_trip_exact"])')"
+: > gpurun_out/resid_lanes.log
+for c in resflow-cond-imagenet64 resflows_smallpatch_split resflow-patches-vqvae; do
+  for v in 1 2; do
+    IDF_LANES=$v timeout -k 10 300 python tools/bench_residual.py --config $c --steps 3 > gpurun_out/r.log 2>&1 || { tail -5 gpurun_out/r.log; exit 1; }
+    echo "$c lanes=$v $(tail -1 gpurun_out/r.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], {k: d[k] for k in d if "ms" in k or "exact" in k})')" | tee -a gpurun_out/resid_lanes.log
+  done
 done
