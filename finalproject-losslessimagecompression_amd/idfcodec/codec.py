@@ -312,6 +312,11 @@ class ImageCodec:
         B = bs.n_images
         bs, word_off, out_state, out_status = self._prep_decode(bs)
         nl = self._n_lanes(B)
+        if nl > 1:
+            try:
+                self._lane_streams(nl)
+            except (OSError, AttributeError, _lib.IdfError):
+                nl = 1  # no separate HIP streams: decode in one lane (same bits)
         h = B // nl
         # the convs must run as the encoder ran them (bit-identical couplings)
         mode, prev = bs.meta.get("conv", "f32"), eng.conv_mode
