@@ -16,3 +16,34 @@ def test_lane_split():
     assert c._n_lanes(256) == 1
     c.lanes = 0
     assert c._n_lanes(256) == 1
+
+
+def test_bench_rans_roofline_accounting():
+    """bench.py's rANS line: algorithmic bytes (12 B/symbol + 4 B/word + 16 B/stream) over the
+    summed launch time, ns per symbol of a stream's chain."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    class Ev:
+        def __init__(self, t):
+            self.t = t
+
+        def elapsed_time(self, other):
+            return other.t - self.t
+
+    class Bs:
+        def total_words(self):
+            return 1000
+
+    # two decode launches of 2 ms each: 100 streams x 3000 symbols
+    trace = [("decode", 300000, 100, Ev(0.0), Ev(2.0)), ("decode", 300000, 100, Ev(5.0), Ev(7.0)),
+             ("encode", 600000, 200, Ev(9.0), Ev(10.0))]
+    r = bench.rans_roofline(trace, Bs(), steps=1)
+    d = r["decode"]
+    assert d["launch_ms_per_step"] == 4.0
+    assert abs(d["ns_per_symbol"] - 4.0e6 / 6000) < 0.1
+    byts = 12.0 * 600000 + 4.0 * 1000 + 16.0 * 200
+    assert abs(d["achieved"] - round(byts / 4e-3 / 1e9, 2)) < 1e-6
+    assert abs(r["encode"]["frac"] - round(r["encode"]["achieved"] / bench.PEAK_HBM_GBS, 5)) < 1e-9
