@@ -1,11 +1,6 @@
-# ad-hoc GPU step (edited per experiment): residual configs with decode lanes 1 vs 2
+# ad-hoc GPU step (edited per experiment): rANS / codec / lanes parity + a 10-step bench
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONDONTWRITEBYTECODE=1
-: > gpurun_out/resid_lanes.log
-for c in resflow-cond-imagenet64 resflows_smallpatch_split resflow-patches-vqvae; do
-  for v in 1 2; do
-    IDF_LANES=$v timeout -k 10 300 python tools/bench_residual.py --config $c --steps 3 > gpurun_out/r.log 2>&1 || { tail -5 gpurun_out/r.log; exit 1; }
-    echo "$c lanes=$v $(tail -1 gpurun_out/r.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], {k: d[k] for k in d if "ms" in k or "exact" in k})')" | tee -a gpurun_out/resid_lanes.log
-  done
-done
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_rans.py tests/test_gpu_codec.py tests/test_gpu_lanes.py > gpurun_out/t_rans.log 2>&1; rc=$?; tail -2 gpurun_out/t_rans.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/b.log 2>&1; rc=$?; tail -1 gpurun_out/b.log | cut -c1-400; exit $rc
