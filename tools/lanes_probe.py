@@ -23,8 +23,8 @@ for _ in range(4):
     assert hip.hipStreamCreateWithFlags(ctypes.byref(h), ctypes.c_uint(1)) == 0
     ext.append(torch.cuda.ExternalStream(h.value))
 torch_streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-V = [(1, "event", "torch", "1"), (1, "event", "torch", "4")]
-V += [(n, st, "ext", w) for n in (2, 4) for st in ("event", "none") for w in ("1", "4")]
+V = [(1, "event", "torch", "4")]
+V += [(2, st, "ext", "4") for st in ("event", "none", "event", "none")]
 for lanes, stg, kind, wpb in V:
     os.environ["IDF_DECODE_WPB"] = wpb
     codec.lanes = lanes
