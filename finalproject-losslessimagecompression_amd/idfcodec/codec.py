@@ -168,6 +168,14 @@ class StreamCoder:
                                      ptr(words)), "gather words")
         return Bitstream(B, shapes, final, nwords, words[:total], status, meta=meta)
 
+    def level_encoder(self, B: int):
+        """Per-level rANS encode overlapped with the flow: forward_pm calls .level(l, ws)
+        once level l's latents and prior are written; that level's streams are encoded on a
+        side stream while the flow computes the next levels (their buffers are disjoint).
+        .finish(ws, compact) joins the side stream and compacts.  The streams are the same
+        launches on the same data as encode(), per level, so the bitstream is identical."""
+        return _LevelEncoder(self, B)
+
     def level_streams(self, B: int, l: int):
         """(first symbol of level l, its symbol count, device int64[B+1] stream offsets
         relative to that first symbol) -- a level's decode touches only its own symbols."""
@@ -204,6 +212,76 @@ class StreamCoder:
             self.trace.append(("decode", nsym, nb, e0, self._mark()))
 
 
+class _LevelEncoder:
+    def __init__(self, coder: StreamCoder, B: int):
+        self.coder, self.B = coder, B
+        eng = coder.engine
+        dev = eng.device
+        self.off = coder.sym_off(B)
+        ns = self.off.numel() - 1
+        self.init = torch.full((ns,), RANS_L, dtype=torch.int64, device=dev)
+        self.final = torch.empty(ns, dtype=torch.int64, device=dev)
+        self.nwords = torch.empty(ns, dtype=torch.int64, device=dev)
+        self.status = torch.empty(ns, dtype=torch.int32, device=dev)
+        if getattr(coder, "_side", None) is None:
+            coder._side = _lib.new_stream(dev)
+        self.side = coder._side
+        self.main = torch.cuda.current_stream(dev)
+        self.scratch = self.wsp = None
+
+    def level(self, l: int, ws):
+        coder, B = self.coder, self.B
+        eng = coder.engine
+        dev = eng.device
+        nsym_all = B * eng.n_sym_img
+        if self.scratch is None:  # on the main stream, before the first side launch
+            sc = ws.get("words")
+            if sc is None or sc.numel() < nsym_all:
+                sc = ws["words"] = torch.empty(nsym_all, dtype=torch.int32, device=dev)
+            self.scratch = sc
+            nmax = B * max(L.n_sym for L in eng.levels)
+            wb = lib().idf_rans_encode_workspace_bytes(nmax)
+            wsp = ws.get("rans_ws")
+            if wsp is None or wsp.numel() < wb:
+                wsp = ws["rans_ws"] = torch.empty(wb, dtype=torch.uint8, device=dev)
+            self.wsp = wsp
+        ev = torch.cuda.Event()
+        ev.record(self.main)
+        self.side.wait_event(ev)
+        base, nsym, rel = coder.level_streams(B, l)
+        k0 = l * B
+        wbytes = lib().idf_rans_encode_workspace_bytes(nsym)
+        with torch.cuda.stream(self.side):
+            s = _lib.stream_ptr(dev)
+            e0 = coder._mark()
+            check(lib().idf_rans_encode_streams(
+                s, B, nsym, ptr(rel), ptr(ws["lat"]) + 4 * base, ptr(ws["mean"]) + 4 * base,
+                ptr(ws["scale"]) + 4 * base, ptr(self.init) + 8 * k0, ptr(self.final) + 8 * k0,
+                ptr(self.scratch) + 4 * base, ptr(self.nwords) + 8 * k0,
+                ptr(self.status) + 4 * k0, ptr(self.wsp), wbytes), "rans encode")
+            if e0 is not None:
+                coder.trace.append(("encode", nsym, B, e0, coder._mark()))
+
+    def finish(self, compact: bool = True) -> Bitstream:
+        self.main.wait_stream(self.side)
+        eng = self.coder.engine
+        B, off, final, nwords, status = self.B, self.off, self.final, self.nwords, self.status
+        scratch = self.scratch
+        shapes = [(L.z, L.h, L.w) for L in eng.levels]
+        meta = {"n_subpixels": B * eng.C * eng.H * eng.W}
+        if not compact:
+            return Bitstream(B, shapes, final, nwords, scratch, status,
+                             meta=dict(meta, scratch_offsets=off[:-1]))
+        ns = off.numel() - 1
+        dst_off = torch.zeros_like(nwords)
+        dst_off[1:] = torch.cumsum(nwords, 0)[:-1]
+        total = int((dst_off[-1] + nwords[-1]).item())
+        words = torch.empty(max(total, 1), dtype=torch.int32, device=eng.device)
+        check(lib().idf_gather_words(_lib.stream_ptr(eng.device), ns, ptr(off), ptr(nwords),
+                                     ptr(dst_off), ptr(scratch), ptr(words)), "gather words")
+        return Bitstream(B, shapes, final, nwords, words[:total], status, meta=meta)
+
+
 class ImageCodec:
     """uint8 NCHW images <-> Bitstream with a FlowEngine (IDFlows configs).
 
@@ -223,6 +301,8 @@ class ImageCodec:
         self.engine = engine
         self.coder = StreamCoder(engine)
         self.lanes = int(os.environ.get("IDF_LANES", "2")) if lanes is None else int(lanes)
+        # per-level rANS encode on a side stream, overlapped with the next levels' flow
+        self.overlap_encode = os.environ.get("IDF_ENC_OVERLAP", "1") == "1"
         self._streams = []
         self.lane_marks = None
 
@@ -243,9 +323,15 @@ class ImageCodec:
         mode = eng.conv_mode
         if mode == "x3":
             eng.clear_range_flag()
-        ws = load()
-        eng.forward_pm(B, cond=cond)
-        bs = self.coder.encode(ws, B, compact=compact)
+        if self.overlap_encode:
+            enc = self.coder.level_encoder(B)
+            load()
+            eng.forward_pm(B, cond=cond, on_level=enc.level)
+            bs = enc.finish(compact=compact)
+        else:
+            ws = load()
+            eng.forward_pm(B, cond=cond)
+            bs = self.coder.encode(ws, B, compact=compact)
         if mode == "x3" and eng.range_flag_tripped():
             eng.set_conv_mode("f32")
             try:

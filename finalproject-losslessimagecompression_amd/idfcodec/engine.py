@@ -398,7 +398,7 @@ class FlowEngine:
 
     # ------------------------------------------------------------ forward
     @torch.no_grad()
-    def forward_pm(self, B: int, cond=None, slot: int = 0):
+    def forward_pm(self, B: int, cond=None, slot: int = 0, on_level=None):
         """Runs flows.py:87-116 from ws['img'] (pixel-major, ld 4) for B images.
         Fills ws lat/mean/logscale/scale.  Returns the workspace."""
         L = lib()
@@ -436,6 +436,8 @@ class FlowEngine:
                 self._top_prior_cached(ws, B, s, o)
             else:
                 self._prior(ws, B, l, s, mean, logs, scale, ptr(x) + Lv.z * FLOAT, Lv.ldx)
+            if on_level is not None:  # level l's lat / mean / scale are final
+                on_level(l, ws)
             src, ld_src, H, W, C = ptr(x) + Lv.z * FLOAT, Lv.ldx, Lv.h, Lv.w, Lv.rest
         return ws
 

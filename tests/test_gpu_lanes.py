@@ -59,3 +59,27 @@ def test_lanes_conditional_decode_identical(golden):
     assert torch.equal(ref, img) and torch.equal(out, img)
     assert torch.equal(info["final_states"], rinfo["final_states"])
     codec.lanes = 2
+
+
+@pytest.mark.parametrize("B", [3, 32])
+def test_overlapped_level_encode_identical(B):
+    """Per-level rANS encode on a side stream (overlapped with the next levels' flow) gives
+    the bitstream of the one-pass encode, compact and not."""
+    from idfcodec import configs, synthetic
+    model = synthetic.build_model(configs.get("imagenet64")).cuda()
+    codec = model.codec()
+    img = synthetic.images(B, seed=70 + B).cuda()
+    codec.overlap_encode = False
+    ref = codec.encode(img)
+    ref_raw = codec.encode(img, compact=False)
+    ref_raw = (ref_raw.states.clone(), ref_raw.nwords.clone(), ref_raw.status.clone())
+    codec.overlap_encode = True
+    got = codec.encode(img)
+    torch.cuda.synchronize()
+    assert torch.equal(got.states, ref.states) and torch.equal(got.nwords, ref.nwords)
+    assert torch.equal(got.words, ref.words)
+    assert torch.equal(got.status, ref.status)
+    raw = codec.encode(img, compact=False)
+    assert torch.equal(raw.states, ref_raw[0]) and torch.equal(raw.nwords, ref_raw[1])
+    out, info = codec.decode(got)
+    assert info["ok"] and torch.equal(out, img)
