@@ -1,18 +1,26 @@
 """bench.py -- encode+decode throughput of the MI355X IDF + rANS lossless codec.
 
 Workload (BASELINE.json configs[1]): configs/imagenet64.yaml, batch 256 of
-synthetic 64x64x3 uint8 images per GPU, fp32 flow (f32-input MFMA) + HIP rANS,
-synthetic seeded weights (no checkpoints exist).  One step = encode
-(dequant -> IDF forward + priors -> per-(image, level) rANS streams ->
-compaction [-> RCCL gather of the shards' bitstreams to rank 0 when N > 1])
-followed by decode (priors -> rANS decode -> IDF inverse -> uint8) of that batch.
-Inputs are resident in HBM before the timed region.  Weak scaling: each rank
-codes its own 256 images; value = all ranks' pixels / max-over-ranks time.
+synthetic 64x64x3 uint8 images per GPU, fp32 flow + HIP rANS, synthetic seeded
+weights (no checkpoints exist).  One step = encode (dequant -> IDF
+forward + priors -> per-(image, level) rANS streams -> compaction) followed by
+decode (priors -> rANS decode -> IDF inverse -> uint8) of that batch.  With N > 1
+GPUs (one process per GPU, RCCL over xGMI) each rank codes its own 256-image shard
+of the global batch and the step also assembles the single-batch bitstream on
+rank 0 (gather_bitstream: a header gather + point-to-point sends) and hands each
+rank its shard of it back for decode (scatter_bitstream) -- the file is what is
+decoded.  Inputs are resident in HBM before the timed region.  Weak scaling:
+value = all ranks' pixels / max-over-ranks time.
+
+`python bench.py --gpus N` with N > 1 and no RANK in the environment starts N
+ranks itself (torch.distributed.run, before anything touches the GPU) and exits
+with their status.
 
 Prints ONE JSON line on rank 0.  Extra keys: encode/decode split, bpp, exact
-round trip, roofline of the dominant kernel (the 3x3-conv implicit-GEMM
-instantiation, timed live with HIP events on its launch stream) and the CPU
-baseline (the oracle: torch-fp32 flow + C rANS on this host's cores).
+round trip, the roofline of the dominant kernel (timed live with HIP events in a
+separate encode pass after the timed steps), the rANS chains, the residual configs
+3-5 (BASELINE configs[2..4]: encode/decode Mpx/s and exactness, one short run each)
+and the CPU baseline (the oracle: torch-fp32 flow + C rANS on this host's cores).
 """
 from __future__ import annotations
 
@@ -42,9 +50,29 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=B_PER_GPU)
-    ap.add_argument("--cpu-baseline-images", type=int, default=16)
+    ap.add_argument("--cpu-baseline-images", type=int, default=64)
+    ap.add_argument("--cpu-baseline-runs", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-residual", action="store_true",
+                    help="skip the residual configs 3-5 extras")
+    ap.add_argument("--launch-probe", action="store_true",
+                    help="ranks report their rank / world size and exit (tests the launcher)")
     return ap.parse_args()
+
+
+def launch(args) -> int:
+    """N ranks of this script under torch.distributed.run (one process per GPU).  The
+    parent never touches the GPU and never execs: it waits and returns the ranks' status."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1", "--master-port",
+           str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd)
 
 
 def pmc_traffic(kernel: str):
@@ -132,11 +160,24 @@ def wino_exec_ratio(eng):
     return 3.0 * r if eng.conv_mode == "x3" else r  # x3: three f16 MFMA passes per product
 
 
-def cpu_baseline(model_cfg, n_img):
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(model_cfg, n_img, runs):
     """The oracle on the host: torch-fp32 flow (oracle/flow_oracle.py) + C rANS
-    (oracle/rans_oracle.c, OpenMP over streams), encode then decode of n_img images.
-    Bounded sample; returns Mpx/s and the thread count used."""
+    (oracle/rans_oracle.c, OpenMP over streams), encode then decode of n_img images, the
+    median of `runs` timed runs after one warm-up.  Bounded sample; returns Mpx/s, the
+    threads used, the CPU model and the host's CPU count."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import statistics
+
     import numpy as np
     import flow_oracle as FO
     import rans_oracle as RO
@@ -147,94 +188,157 @@ def cpu_baseline(model_cfg, n_img):
     img = synthetic.images(n_img, seed=7)
     threads = torch.get_num_threads()
     o.forward(FO.dequant(img[:1]))  # warm-up (oneDNN primitive creation)
-    t0 = time.perf_counter()
-    x = FO.dequant(img)
-    lat, me, ls = o.forward(x)
-    flat = lambda ts: np.concatenate([t.reshape(-1).numpy() for t in ts])  # noqa: E731
-    L = flat(lat)
-    M = flat(me)
-    S = flat([torch.exp(t) for t in ls])
-    sizes = [t[0].numel() for t in lat]
-    off = [0]
-    for n in sizes:
-        off += [off[-1] + n * (b + 1) for b in range(n_img)]
-    off = np.asarray(off, np.int64)
-    fs, words, nw, st = RO.encode_streams(off, L, M, S)
-    t_enc = time.perf_counter() - t0
-    level_base = [0]
-    for n in sizes:
-        level_base.append(level_base[-1] + n * n_img)
 
-    def dec(l, m, s):
-        k0 = l * n_img
-        sl = slice(k0, k0 + n_img)
-        o_l = off[k0:k0 + n_img + 1] - off[k0]
-        m_np = m.reshape(-1).numpy()
-        s_np = torch.exp(s).reshape(-1).numpy()
-        w_off = off[k0:k0 + n_img]
-        fs2, out, st2 = RO.decode_streams(o_l, w_off, nw[sl], words, m_np, s_np, fs[sl])
-        return torch.from_numpy(out).view(m.shape)
+    def once():
+        t0 = time.perf_counter()
+        x = FO.dequant(img)
+        lat, me, ls = o.forward(x)
+        flat = lambda ts: np.concatenate([t.reshape(-1).numpy() for t in ts])  # noqa: E731
+        L = flat(lat)
+        M = flat(me)
+        S = flat([torch.exp(t) for t in ls])
+        sizes = [t[0].numel() for t in lat]
+        off = [0]
+        for n in sizes:
+            off += [off[-1] + n * (b + 1) for b in range(n_img)]
+        off = np.asarray(off, np.int64)
+        fs, words, nw, st = RO.encode_streams(off, L, M, S)
+        t_enc = time.perf_counter() - t0
 
-    t1 = time.perf_counter()
-    xd, _ = o.decode_levels(n_img, dec)
-    t_dec = time.perf_counter() - t1
-    exact = bool(torch.equal(xd, x))
+        def dec(l, m, s):
+            k0 = l * n_img
+            sl = slice(k0, k0 + n_img)
+            o_l = off[k0:k0 + n_img + 1] - off[k0]
+            m_np = m.reshape(-1).numpy()
+            s_np = torch.exp(s).reshape(-1).numpy()
+            w_off = off[k0:k0 + n_img]
+            fs2, out, st2 = RO.decode_streams(o_l, w_off, nw[sl], words, m_np, s_np, fs[sl])
+            return torch.from_numpy(out).view(m.shape)
+
+        t1 = time.perf_counter()
+        xd, _ = o.decode_levels(n_img, dec)
+        t_dec = time.perf_counter() - t1
+        return t_enc, t_dec, bool(torch.equal(xd, x))
+
+    res = [once() for _ in range(max(1, runs))]
+    tot = [a + b for a, b, _ in res]
+    med = statistics.median(tot)
+    t_enc, t_dec, _ = res[tot.index(sorted(tot)[len(tot) // 2])]
+    exact = all(e for _, _, e in res)
     px = n_img * PX_PER_IMG
-    return {"value": round(px / (t_enc + t_dec) / 1e6, 5), "unit": "Mpx/s", "cores": threads,
-            "kind": "port",
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count()
+    return {"value": round(px / med / 1e6, 5), "unit": "Mpx/s", "cores": threads,
+            "kind": "port", "cpu_model": _cpu_model(), "host_nproc": os.cpu_count(),
+            "affinity_cpus": avail, "runs": len(res),
+            "runs_mpx_s": [round(px / t / 1e6, 5) for t in tot],
             "sample": (f"{n_img} synthetic 64x64 images, imagenet64 model, encode+decode "
-                       f"(torch-fp32 flow oracle, {threads} threads + C rANS oracle); "
-                       f"enc {t_enc:.2f}s dec {t_dec:.2f}s, round trip exact={exact}")}
+                       f"(torch-fp32 flow oracle, {threads} threads + C rANS oracle), median of "
+                       f"{len(res)} runs; median run enc {t_enc:.2f}s dec {t_dec:.2f}s, "
+                       f"round trips exact={exact}")}
+
+
+def roofline_pass(codec, eng, timer, img):
+    """The dominant kernel timed live: one encode of the batch after the timed steps, with the
+    side-stream rANS encode off (every conv launch has the chip to itself) and HIP events
+    around every DenseLayer conv launch of every coupling and prior (idf_dense_block_f32_timed
+    brackets each launch on the stream it is issued on).  Returns (achieved TF/s,
+    average launch ms, launches, algorithmic FLOPs per launch)."""
+    import ctypes
+    from idfcodec import _lib
+    for b in eng._blocks:
+        b.timer = timer
+    prev = codec.overlap_encode
+    codec.overlap_encode = False
+    _lib.lib().idf_timer_reset(timer)
+    try:
+        codec.encode(img)
+        torch.cuda.synchronize()
+    finally:
+        codec.overlap_encode = prev
+        for b in eng._blocks:
+            b.timer = None
+    tot, cnt, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+    _lib.check(_lib.lib().idf_timer_summary(timer, _lib.TAG_CONV3X3, ctypes.byref(tot),
+                                            ctypes.byref(cnt), ctypes.byref(fl)), "timer")
+    n = max(cnt.value, 1)
+    tflops = fl.value / (tot.value * 1e-3) / 1e12 if tot.value > 0 else 0.0
+    return tflops, tot.value / n, cnt.value, fl.value / n
+
+
+def residual_extras(args):
+    """BASELINE configs[2..4] (the residual VQ-VAE + flow codecs): one short run each on this
+    rank's GPU (sharded per rank when N > 1, bitstreams gathered to rank 0 in the timed
+    encode), reported beside the headline."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import bench_residual
+    out = {}
+    for name in ("resflow-cond-imagenet64", "resflows_smallpatch_split", "resflow-patches-vqvae"):
+        try:
+            r = bench_residual.run(name, steps=2, warmup=1)
+        except Exception as e:  # reported, never hides the headline
+            r = {"error": repr(e)}
+            if dist.is_initialized():
+                raise
+        if r is not None:
+            out[name] = {k: r[k] for k in ("value", "encode_mpx_s", "decode_mpx_s", "encode_ms",
+                                           "decode_ms", "batch_per_gpu", "image", "bpp",
+                                           "round_trip_exact", "dtype", "n_gpus") if k in r} \
+                if "error" not in r else r
+    return out
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "RANK" not in os.environ:
+        return launch(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_probe:  # no GPU work: the launcher test
+        print(json.dumps({"rank": rank, "world": world, "local_rank": local}), flush=True)
+        return 0
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        assert dist.get_world_size() == args.gpus, "process group size != --gpus"
 
     from idfcodec import _lib, configs, synthetic
-    from idfcodec.dist import gather_streams
+    from idfcodec.dist import broadcast_state, gather_bitstream, scatter_bitstream, shard_range
 
     cfg = configs.get("imagenet64")
     model = synthetic.build_model(cfg).to(dev)
+    if world > 1:
+        broadcast_state(model)  # replicated weights: one broadcast from rank 0
     codec = model.codec()
     eng = model.engine()
     B = args.batch
-    img = synthetic.images(B, seed=2 + rank).to(dev)
+    lo, hi = shard_range(B * world, rank, world)
+    img = synthetic.images(B * world, seed=2)[lo:hi].to(dev)  # this rank's shard
 
-    # live kernel timing on the dominant kernel (sampled: coupling 0 of every level)
-    timer = _lib.lib().idf_timer_create(4096)
-    sampled = [eng.couple[l][0] for l in range(eng.nsplit)]
-
-    def step(timed=False):
-        for b in sampled:
-            b.timer = timer if timed else None
+    def step():
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e2 = torch.cuda.Event(enable_timing=True)
         e0.record()
         bs = codec.encode(img)
+        full = None
         if world > 1:
-            gather_streams(bs.states, bs.nwords, bs.words, dst=0)
+            full = gather_bitstream(bs, dst=0)  # the single-batch file on rank 0
+            bs, _ = scatter_bitstream(full, src=0, device=dev)  # decode what the file holds
         e1.record()
-        # the conv roofline is sampled on the encode pass: there every launch has the chip to
-        # itself, while the decode lanes overlap two half-batch launches (their event-bracketed
-        # durations would include each other's time)
-        for b in sampled:
-            b.timer = None
         out, info = codec.decode(bs, verify=False)
         e2.record()
-        return bs, out, (e0, e1, e2)
+        return bs, full, out, (e0, e1, e2)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    _lib.lib().idf_timer_reset(timer)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -242,7 +346,7 @@ def main():
     t0 = time.perf_counter()
     evs = []
     for _ in range(args.steps):
-        bs, out, ev = step(timed=True)
+        bs, full, out, ev = step()
         evs.append(ev)
     torch.cuda.synchronize()
     if world > 1:
@@ -258,22 +362,23 @@ def main():
     enc_ms = sum(a.elapsed_time(b) for a, b, _ in evs) / len(evs)
     dec_ms = sum(b.elapsed_time(c) for _, b, c in evs) / len(evs)
 
-    # exactness of the last timed step
-    exact = bool(torch.equal(out, img))
-    bpp = 3.0 * bs.bpd()
+    # exactness of the last timed step on every rank (and, N > 1, of the whole gathered
+    # single-batch bitstream decoded on rank 0 alone, below)
+    ok = torch.tensor([1 if torch.equal(out, img) else 0], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    exact = bool(ok.item())
+    full_exact = None
+    if world > 1 and rank == 0:
+        whole = synthetic.images(B * world, seed=2).to(dev)
+        img_full, info = codec.decode(full)
+        full_exact = bool(info["ok"]) and bool(torch.equal(img_full, whole))
+        del whole, img_full
+    bits = full.bits() if full is not None else bs.bits()
+    bpp = 3.0 * bits / (3 * B * world * PX_PER_IMG)
 
-    import ctypes
-    tot = ctypes.c_double()
-    cnt = ctypes.c_int64()
-    fl = ctypes.c_double()
-    _lib.check(_lib.lib().idf_timer_summary(timer, _lib.TAG_CONV3X3, ctypes.byref(tot),
-                                            ctypes.byref(cnt), ctypes.byref(fl)), "timer")
-    c3_avg_ms = tot.value / max(cnt.value, 1)
-    c3_tflops = fl.value / (tot.value * 1e-3) / 1e12 if tot.value > 0 else 0.0
-    _lib.check(_lib.lib().idf_timer_summary(timer, _lib.TAG_CONV1X1, ctypes.byref(tot),
-                                            ctypes.byref(cnt), ctypes.byref(fl)), "timer")
-    c1_tflops = fl.value / (tot.value * 1e-3) / 1e12 if tot.value > 0 else 0.0
-    c1_avg_ms = tot.value / max(cnt.value, 1)
+    timer = _lib.lib().idf_timer_create(8192)
+    c3_tflops, c3_avg_ms, c3_n, c3_flops = roofline_pass(codec, eng, timer, img)
     _lib.lib().idf_timer_destroy(timer)
 
     flops = eng.flops_per_image()["total"]
@@ -282,15 +387,25 @@ def main():
     traffic, traffic_src = pmc_traffic(kname) if eng.wino else (None, None)
     # the x3 kernel's products run on f16 MFMA: price them against the f16 dense peak
     peak = PEAK_F16_TFLOPS if (eng.wino and eng.conv_mode == "x3") else PEAK_F32_TFLOPS
+    flops_exec = eng.flops_per_image(fold=eng.fold)["total"]
+    fold, conv_mode, kdesc, exec_ratio = eng.fold, eng.conv_mode, conv_kernel_name(eng), \
+        wino_exec_ratio(eng)
     step_ms = elapsed / args.steps * 1e3
     px_total = world * B * PX_PER_IMG * args.steps
     value = px_total / elapsed / 1e6
+
+    residual = None
+    if not args.no_residual:
+        del codec, eng, model, img, out, bs, full
+        torch.cuda.empty_cache()
+        residual = residual_extras(args)
+
     result = None
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             try:
-                cpu = cpu_baseline(cfg, args.cpu_baseline_images)
+                cpu = cpu_baseline(cfg, args.cpu_baseline_images, args.cpu_baseline_runs)
             except Exception as e:  # the baseline is reported, never the product
                 cpu = {"value": None, "error": repr(e)}
         result = {
@@ -309,7 +424,10 @@ def main():
             "config": {"workload": "configs/imagenet64.yaml, batch 256 x 64x64x3 uint8 per GPU, "
                                    "fp32 flow + HIP rANS (BASELINE configs[1])",
                        "global_batch": world * B, "parallelism": f"dp{world} (batch shards)",
-                       "streams_per_gpu": 3 * B},
+                       "streams_per_gpu": 3 * B,
+                       "multi_gpu_step": ("encode shard -> gather_bitstream to rank 0 -> "
+                                          "scatter_bitstream -> decode shard"
+                                          if world > 1 else "encode -> decode")},
             "encode_mpx_s": round(B * PX_PER_IMG / enc_ms / 1e3, 4),
             "decode_mpx_s": round(B * PX_PER_IMG / dec_ms / 1e3, 4),
             "encode_ms": round(enc_ms, 3),
@@ -317,39 +435,41 @@ def main():
             "bpp": round(bpp, 4),
             "bits_per_subpixel": round(bpp / 3, 4),
             "round_trip_exact": exact,
+            "gathered_bitstream_exact": full_exact,
             "flow_tflops_per_direction": round(B * flops / 1e12, 4),
-            "flow_tflops_executed_per_direction": round(
-                B * eng.flops_per_image(fold=eng.fold)["total"] / 1e12, 4),
-            "fold_1x1_into_3x3": eng.fold,
+            "flow_tflops_executed_per_direction": round(B * flops_exec / 1e12, 4),
+            "fold_1x1_into_3x3": fold,
             "roofline": {
-                "kernel": conv_kernel_name(eng),
+                "kernel": kdesc,
                 "flops_per_launch": "2*P*9*c*g (P = B*h*w pixels, c/g unpadded in/out "
-                                    "channels of the layer; averaged over the sampled launches)",
-                "sampled": "coupling 0 of every level, encode pass of every timed step",
+                                    "channels of the layer)",
+                "algorithmic_gflop_per_launch": round(c3_flops / 1e9, 3),
+                "sampled": ("every DenseLayer conv launch (8 couplings + prior, every level) of "
+                            "one encode after the timed steps, side-stream rANS encode off"),
+                "launches": c3_n,
                 "bound": "mfma",
                 "achieved": round(c3_tflops, 3),
                 "peak": peak,
                 "unit": "TFLOP/s",
                 "frac": round(c3_tflops / peak, 4),
-                "conv_mode": eng.conv_mode,
+                "conv_mode": conv_mode,
                 "traffic": traffic,
                 "traffic_unit": "B/launch (HBM, PMC)",
                 "traffic_source": traffic_src,
                 "avg_launch_ms": round(c3_avg_ms, 5),
-                "mfma_executed_tflops": round(c3_tflops * wino_exec_ratio(eng), 3),
-                "mfma_executed_frac": round(c3_tflops * wino_exec_ratio(eng) / peak, 4),
-                "conv1x1_achieved": round(c1_tflops, 3),
-                "conv1x1_avg_launch_ms": round(c1_avg_ms, 5),
+                "mfma_executed_tflops": round(c3_tflops * exec_ratio, 3),
+                "mfma_executed_frac": round(c3_tflops * exec_ratio / peak, 4),
             },
             "rans": rans,
+            "residual_configs": residual,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    return result
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

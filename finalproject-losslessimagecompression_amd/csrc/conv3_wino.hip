@@ -1155,13 +1155,6 @@ static WinoPlan wino_plan(int H, int W, int nslab, int N) {
   // and reduce then cost more than they gain (measured: config 4 5.4 -> 8.3 Mpx/s, config 3's
   // VQ-VAE 67 -> 54 ms; imagenet64's 8x8 level keeps 4: 10.2 vs 9.6 Mpx/s with 1).
   if (pl.big || N > 64) pl.ksplit = 1;
-  {  // timing experiments only: cap the split (IDF_WINO_KSPLIT_MAX)
-    static const int cap = [] {
-      const char* e = getenv("IDF_WINO_KSPLIT_MAX");
-      return e ? atoi(e) : 0;
-    }();
-    if (cap > 0 && pl.ksplit > cap) pl.ksplit = cap;
-  }
   if (pl.ksplit > nslab) pl.ksplit = nslab > 0 ? nslab : 1;
   pl.ok = 1;
   return pl;

@@ -382,6 +382,47 @@ __global__ void dequant_u8_kernel(int B, int C, int H, int W, const uint8_t* __r
   out[(b * hw + pix) * ld + c] = (float)(k + (k >= 128 ? 1 : 0)) * (1.0f / 256.0f);
 }
 
+// ------------------------------------------------------------------ log-likelihood
+// DLogistic.log_prob (distlib.py:40-55) per symbol, with IDFlows.log_likelihood's per-image
+// reduction (flows.py:154-169) fused: one block per (level, image) group reduces its
+// group_len log-probabilities in a fixed order (per-thread strided f64 partials, then a fixed
+// tree), so the sums are deterministic.  The per-symbol arithmetic follows torch's fp32 ops
+// in the reference's order: scale = exp(logscale); x+- = ((x +- 0.5/bins) - mean) / scale;
+// logsigmoid(v) = min(v, 0) - log1p(exp(-|v|)); logP = lp + log((1 - exp(ln - lp)) + eps).
+__device__ __forceinline__ float idf_logsigmoid(float v) {
+  return fminf(v, 0.0f) - log1pf(expf(-fabsf(v)));
+}
+
+__global__ void __launch_bounds__(256) log_prob_kernel(int64_t group_len,
+                                                       const float* __restrict__ x,
+                                                       const float* __restrict__ mean,
+                                                       const float* __restrict__ logscale,
+                                                       float half_bin, float eps,
+                                                       float* __restrict__ logp,
+                                                       double* __restrict__ gsum) {
+  const int64_t g0 = (int64_t)blockIdx.x * group_len;
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < group_len; i += 256) {
+    const int64_t k = g0 + i;
+    const float sc = expf(logscale[k]);
+    const float xm = x[k], mu = mean[k];
+    const float xp = ((xm + half_bin) - mu) / sc;
+    const float xn = ((xm - half_bin) - mu) / sc;
+    const float lp = idf_logsigmoid(xp), ln = idf_logsigmoid(xn);
+    const float v = lp + logf((1.0f - expf(ln - lp)) + eps);
+    if (logp) logp[k] = v;
+    acc += (double)v;
+  }
+  __shared__ double red[256];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && gsum) gsum[blockIdx.x] = red[0];
+}
+
 __global__ void quant_u8_kernel(int B, int C, int H, int W, const float* __restrict__ in, int64_t ld,
                                 uint8_t* __restrict__ img, int32_t* __restrict__ bad) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -684,6 +725,19 @@ int idf_dequant_u8(void* stream, int32_t B, int32_t C, int32_t H, int32_t W, con
   if (n <= 0) return n < 0 ? IDF_ERR_ARG : IDF_OK;
   hipLaunchKernelGGL(dequant_u8_kernel, grid1d(n), dim3(256), 0, (hipStream_t)stream, B, C, H, W,
                      img, out, ld_out);
+  return idf_last_error();
+}
+
+int idf_log_prob(void* stream, int64_t n_groups, int64_t group_len, const float* x,
+                 const float* mean, const float* logscale, int32_t nbits, float eps,
+                 float* logp, double* group_sum) {
+  if (n_groups < 0 || group_len < 0 || nbits < 0 || nbits > 30) return IDF_ERR_ARG;
+  if (n_groups == 0) return IDF_OK;
+  if (n_groups > 0x7fffffff || !x || !mean || !logscale) return IDF_ERR_ARG;
+  const float half_bin = 0.5f / (float)(1 << nbits);
+  hipLaunchKernelGGL(log_prob_kernel, dim3((unsigned)n_groups), dim3(256), 0,
+                     (hipStream_t)stream, group_len, x, mean, logscale, half_bin, eps, logp,
+                     group_sum);
   return idf_last_error();
 }
 

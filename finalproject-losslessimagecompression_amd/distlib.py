@@ -5,7 +5,6 @@ idfcodec/csrc/idf_cdf.h).  BinomialDistribution / UnitGaussianDistribution are
 VQ-VAE training losses (distlib.py:73-101); they are registered so the residual
 configs construct, and compute with torch.distributions (not a coding path)."""
 import torch
-import torch.nn.functional as F
 from torch import nn
 
 import moduleregister
@@ -23,6 +22,22 @@ class Distribution(nn.Module):
         super().__init__()
 
 
+def dlogistic_log_prob(x, mean, logscale, nbits=8, eps=1e-8, groups=1, logp=None):
+    """idf_log_prob over contiguous fp32 device tensors split into `groups` equal groups:
+    fills `logp` (if given) and returns the per-group f64 sums (fixed-order reduction)."""
+    from idfcodec import _lib
+    from idfcodec._lib import check, lib, ptr
+    x, mean, logscale = (t.contiguous().float() for t in (x, mean, logscale))
+    n = x.numel()
+    if n % max(groups, 1):
+        raise ValueError("log_prob groups must divide the element count")
+    sums = torch.empty(groups, dtype=torch.float64, device=x.device)
+    check(lib().idf_log_prob(_lib.stream_ptr(x.device), groups, n // max(groups, 1), ptr(x),
+                             ptr(mean), ptr(logscale), int(nbits), float(eps),
+                             ptr(logp) if logp is not None else None, ptr(sums)), "log_prob")
+    return sums
+
+
 @NNDistribution.register
 class DLogistic(Distribution):
     def __init__(self, round=None):
@@ -34,13 +49,13 @@ class DLogistic(Distribution):
             self.round = Round()
 
     def log_prob(self, x, mean, logscale, nbits=8, eps=1e-8):
+        """distlib.py:40-55 on the device (idf_log_prob): elementwise, broadcasting as the
+        reference's torch ops do."""
         require_device(x, "DLogistic input")
-        scale = torch.exp(logscale)
-        bins = 2 ** nbits
-        x_pos = (x + 0.5 / bins - mean) / scale
-        x_neg = (x - 0.5 / bins - mean) / scale
-        lp, ln = F.logsigmoid(x_pos), F.logsigmoid(x_neg)
-        return lp + torch.log(1 - torch.exp(ln - lp) + eps)
+        x, mean, logscale = torch.broadcast_tensors(x, mean, logscale)
+        out = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+        dlogistic_log_prob(x, mean, logscale, nbits, eps, logp=out)
+        return out
 
     def sample(self, mean, logscale, nbits=8):
         u = torch.rand_like(mean)

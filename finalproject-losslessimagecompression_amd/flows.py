@@ -146,15 +146,22 @@ class IDFlows(nn.Module):
         return eng.image_nchw(ws, B)
 
     def log_likelihood(self, latents, means, logscales):
-        """flows.py:154-169."""
+        """flows.py:154-169: per image, the log-probabilities of every level summed (per-level
+        means in log_Ps), divided by H*W*C -- one idf_log_prob launch per level, the
+        per-(level, image) sums reduced on the device in a fixed order (f64)."""
+        from distlib import DLogistic, dlogistic_log_prob
+        if not isinstance(self.dist, DLogistic):
+            raise NotImplementedError("log_likelihood supports the DLogistic prior only")
+        B = latents[0].shape[0]
+        dev = latents[0].device
+        require_device(latents[0], "latents")
+        total = torch.zeros(B, dtype=torch.float64, device=dev)
         log_Ps = []
-        log_prob = torch.zeros((latents[0].shape[0],), device=latents[0].device)
         for z, m, ls in zip(latents, means, logscales):
-            logp = self.dist.log_prob(z, m, ls, self.nbits)
-            log_Ps.append(torch.mean(logp, dim=(1, 2, 3)))
-            log_prob += torch.sum(logp, dim=(1, 2, 3))
-        log_prob /= (self.H * self.W * self.C)
-        return log_prob, log_Ps
+            sums = dlogistic_log_prob(z.to(dev), m.to(dev), ls.to(dev), self.nbits, groups=B)
+            log_Ps.append((sums / (z.numel() // B)).float())
+            total += sums
+        return (total / (self.H * self.W * self.C)).float(), log_Ps
 
     def inverse(self):
         for block in self.blocks:

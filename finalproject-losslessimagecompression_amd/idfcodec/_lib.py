@@ -76,6 +76,7 @@ SIGNATURES = {
     "idf_gather_words": (ctypes.c_int, [P, i64, P, P, P, P, P]),
     "idf_rans_encode": (ctypes.c_int, [P, i64, P, P, P, P, P, P]),
     "idf_rans_decode": (ctypes.c_int, [P, P, i64, i64, P, P, P, P]),
+    "idf_log_prob": (ctypes.c_int, [P, i64, i64, P, P, P, i32, f32, P, P]),
     "idf_expf_glibc": (ctypes.c_int, [P, i64, P, P]),
     "idf_expf_checksum": (ctypes.c_int, [P, u64, u64, P]),
     "idf_rans_cdf_selfcheck": (ctypes.c_int, [P, u64, u64, P]),

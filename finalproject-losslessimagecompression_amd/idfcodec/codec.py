@@ -27,6 +27,10 @@ RANS_L = 1 << 32
 MAGIC = b"IDFB"
 VERSION = 1
 FLAG_CONV_X3 = 1
+# container flags bits 0-3: the conv arithmetic the flow ran (engine.conv_family); the decoder
+# must run the same one.  0 = exact-f32 Winograd (every stream written before the field existed)
+CONV_CODES = {"f32": 0, "x3": 1, "halo": 2, "gemm": 3, "unfold": 4, "bf16": 5}
+CONV_NAMES = {v: k for k, v in CONV_CODES.items()}
 
 
 @dataclass
@@ -70,7 +74,10 @@ class Bitstream:
     def to_bytes(self) -> bytes:
         # flags bit 0: the flow's Winograd convs ran as split-f16 products (meta conv 'x3');
         # 0: exact-f32 (every stream written before the flag existed)
-        flags = FLAG_CONV_X3 if self.meta.get("conv", "f32") == "x3" else 0
+        conv = self.meta.get("conv", "f32")
+        if conv not in CONV_CODES:
+            raise ValueError(f"unknown conv mode {conv!r}")
+        flags = CONV_CODES[conv]
         hdr = struct.pack("<4sHHIII", MAGIC, VERSION, flags, self.n_images, len(self.level_shapes),
                           self.n_streams)
         shapes = b"".join(struct.pack("<III", *s) for s in self.level_shapes)
@@ -96,9 +103,10 @@ class Bitstream:
         o += 4 * n_str
         w = np.frombuffer(buf, "<i4", int(nw.sum()), o).copy()
         t = lambda a: torch.from_numpy(a).to(device) if device else torch.from_numpy(a)  # noqa: E731
+        if (flags & 0xF) not in CONV_NAMES or flags >> 4:
+            raise ValueError(f"unknown bitstream flags {flags:#x}")
         return cls(n_img, [tuple(s) for s in shapes], t(st), t(nw), t(w),
-                   meta={"n_subpixels": int(nsub),
-                         "conv": "x3" if flags & FLAG_CONV_X3 else "f32"})
+                   meta={"n_subpixels": int(nsub), "conv": CONV_NAMES[flags & 0xF]})
 
 
 class StreamCoder:
@@ -228,6 +236,11 @@ class _LevelEncoder:
         self.side = coder._side
         self.main = torch.cuda.current_stream(dev)
         self.scratch = self.wsp = None
+        # every level's stream offsets are built here, on the main stream, before the first
+        # event the side stream waits on: built lazily inside level() they would be written
+        # after that event and the side-stream encode could read them unwritten
+        for l in range(len(eng.levels)):
+            coder.level_streams(B, l)
 
     def level(self, l: int, ws):
         coder, B = self.coder, self.B
@@ -245,10 +258,10 @@ class _LevelEncoder:
             if wsp is None or wsp.numel() < wb:
                 wsp = ws["rans_ws"] = torch.empty(wb, dtype=torch.uint8, device=dev)
             self.wsp = wsp
+        base, nsym, rel = coder.level_streams(B, l)  # cached in __init__: no launch here
         ev = torch.cuda.Event()
         ev.record(self.main)
         self.side.wait_event(ev)
-        base, nsym, rel = coder.level_streams(B, l)
         k0 = l * B
         wbytes = lib().idf_rans_encode_workspace_bytes(nsym)
         with torch.cuda.stream(self.side):
@@ -262,8 +275,12 @@ class _LevelEncoder:
             if e0 is not None:
                 coder.trace.append(("encode", nsym, B, e0, coder._mark()))
 
-    def finish(self, compact: bool = True) -> Bitstream:
+    def join(self):
+        """The main stream waits for every side-stream launch issued so far."""
         self.main.wait_stream(self.side)
+
+    def finish(self, compact: bool = True) -> Bitstream:
+        self.join()
         eng = self.coder.engine
         B, off, final, nwords, status = self.B, self.off, self.final, self.nwords, self.status
         scratch = self.scratch
@@ -320,13 +337,23 @@ class ImageCodec:
         beyond its f16 range), recompute the batch with the exact-f32 convs.  The mode that
         produced the streams is recorded in the bitstream (meta['conv'], container flag)."""
         eng = self.engine
-        mode = eng.conv_mode
+        mode = eng.conv_family
         if mode == "x3":
             eng.clear_range_flag()
+        enc = None
         if self.overlap_encode:
-            enc = self.coder.level_encoder(B)
+            try:
+                enc = self.coder.level_encoder(B)
+            except (OSError, AttributeError, _lib.IdfError):
+                # no separate HIP stream available: the one-pass encode (same bitstream)
+                self.overlap_encode = False
+        if enc is not None:
             load()
-            eng.forward_pm(B, cond=cond, on_level=enc.level)
+            try:
+                eng.forward_pm(B, cond=cond, on_level=enc.level)
+            finally:
+                # never free or reuse main-stream buffers while side launches may run
+                enc.join()
             bs = enc.finish(compact=compact)
         else:
             ws = load()
@@ -377,7 +404,39 @@ class ImageCodec:
             self._streams.append(_lib.new_stream(self.engine.device))
         return self._streams[:n]
 
+    def check_bitstream(self, bs: Bitstream):
+        """Raises ValueError unless bs was produced by an engine of this geometry: the
+        rANS decode indexes streams, word offsets and states by (level, image), so a
+        truncated or foreign container would otherwise read device memory out of bounds."""
+        eng = self.engine
+        want = [(L.z, L.h, L.w) for L in eng.levels]
+        if [tuple(int(v) for v in s) for s in bs.level_shapes] != want:
+            raise ValueError(f"bitstream level shapes {bs.level_shapes} do not match the "
+                             f"model's {want}")
+        if bs.n_images < 0 or bs.n_streams != len(eng.levels) * bs.n_images:
+            raise ValueError(f"bitstream holds {bs.n_streams} streams, expected "
+                             f"{len(eng.levels)} levels x {bs.n_images} images")
+        if bs.nwords.numel() != bs.n_streams:
+            raise ValueError("bitstream word-count table does not match its stream count")
+        if bool((bs.nwords < 0).any().item()):
+            raise ValueError("bitstream has a negative word count")
+        if "scratch_offsets" not in bs.meta:
+            total = int(bs.nwords.sum().item()) if bs.n_streams else 0
+            if total != bs.words.numel():
+                raise ValueError(f"bitstream word table sums to {total} words, "
+                                 f"{bs.words.numel()} present")
+        conv, have = bs.meta.get("conv", "f32"), eng.conv_family
+        if conv not in CONV_CODES:
+            raise ValueError(f"unknown conv mode {conv!r}")
+        switchable = conv in ("x3", "f32") and have in ("x3", "f32") and (conv == "f32" or
+                                                                          eng.wx3)
+        if conv != have and not switchable:
+            raise ValueError(f"bitstream was coded with {conv!r} convs; this engine runs "
+                             f"{have!r} (IDF_FOLD / IDF_WINO / IDF_HALO / precision differ): "
+                             "its couplings would not invert bit-exactly")
+
     def _prep_decode(self, bs: Bitstream):
+        self.check_bitstream(bs)
         dev = self.engine.device
         if bs.states.device != dev:
             bs = Bitstream(bs.n_images, bs.level_shapes, bs.states.to(dev), bs.nwords.to(dev),
@@ -406,6 +465,8 @@ class ImageCodec:
         h = B // nl
         # the convs must run as the encoder ran them (bit-identical couplings)
         mode, prev = bs.meta.get("conv", "f32"), eng.conv_mode
+        if mode not in ("x3", "f32"):  # a fixed family, checked equal in check_bitstream
+            mode = prev
         if mode != prev:
             eng.set_conv_mode(mode)
         try:

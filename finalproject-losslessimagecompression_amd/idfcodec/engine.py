@@ -267,6 +267,20 @@ class FlowEngine:
         self.conv_mode = mode
         self._top_prior = None  # computed under the previous mode
 
+    @property
+    def conv_family(self) -> str:
+        """Which conv arithmetic produces the couplings -- the decoder must run the same one
+        (Bitstream.meta['conv']): 'x3' / 'f32' (Winograd split-f16 / exact f32, switchable
+        per bitstream), 'bf16', 'halo' (direct LDS-halo kernel), 'gemm' (folded implicit
+        GEMM) or 'unfold' (the reference's 1x1 + 3x3, IDF_FOLD=0)."""
+        if self.precision == "bf16":
+            return "bf16"
+        if not self.fold:
+            return "unfold"
+        if self.wino:
+            return self.conv_mode
+        return "halo" if HALO else "gemm"
+
     def clear_range_flag(self):
         self.range_flag.zero_()
 

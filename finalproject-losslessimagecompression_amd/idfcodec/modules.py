@@ -66,22 +66,35 @@ def _feat_from_nchw(x, db: DeviceBlock, extra_cols=0):
 def run_dense_block(block, x: torch.Tensor, fold=None) -> torch.Tensor:
     """DenseBlock.forward (nnblock.py:53-56) -> NCHW [B, o_channel, H, W]."""
     require_device(x, "DenseBlock input")
-    db = device_block(block, x.device, fold)
+    return run_device_block(device_block(block, x.device, fold), x)[0]
+
+
+@torch.no_grad()
+def run_device_block(db: DeviceBlock, x: torch.Tensor, return_feat: bool = False):
+    """A packed DeviceBlock -- e.g. one of a FlowEngine's own coupling / prior blocks, in
+    the engine's conv mode -- over NCHW input x: (head output NCHW [B, n_head, H, W], the
+    pixel-major feature buffer [P, ld_feat] holding the input and every layer's output, or
+    None unless return_feat)."""
+    require_device(x, "DenseBlock input")
     B, C, H, W = x.shape
     feat, ld, s = _feat_from_nchw(x, db)
-    tmp = torch.empty_like(feat)
+    P = B * H * W
+    ld_tmp = ld
+    if db.desc.bf16:  # bf16 shadow of the features ahead of the split-K partials
+        ld_tmp = max(ld, round_up(ld, 64) // 2 + 2 * 48 + 8)
+    tmp = torch.empty(P * ld_tmp, dtype=torch.float32, device=x.device)
     n = db.geom.n_head
     ldo = round_up(n, 4)
     out_pm = torch.empty(B * H * W * ldo, dtype=torch.float32, device=x.device)
     check(lib().idf_dense_block_f32(s, ctypes.byref(db.desc), B, H, W, ptr(feat), ld,
-                                    ptr(tmp), ld, None), "dense block")
+                                    ptr(tmp), ld_tmp, None), "dense block")
     # head=NULL skips the head inside the block call; run it with a plain store epilogue
     check(lib().idf_conv1x1_f32(s, B * H * W, db.geom.width, n, ptr(feat), ld, ptr(db.wh),
                                 db.packed.ldwh, db.packed.nh_alloc, ptr(db.bh), ptr(out_pm), ldo, B,
                                 H, W, None), "head")
     out = torch.empty((B, n, H, W), dtype=torch.float32, device=x.device)
     check(lib().idf_pm_to_nchw(s, B, n, H, W, ptr(out_pm), ldo, ptr(out)), "pm_to_nchw")
-    return out
+    return out, (feat.view(P, ld) if return_feat else None)
 
 
 @torch.no_grad()

@@ -327,6 +327,16 @@ int idf_f32_to_bf16_cols(void *stream, int64_t P, int32_t n, int32_t n_zero, con
  * out[p, c] = (k + [k >= 128]) / 256 == rint(k/255*256)/256. */
 int idf_dequant_u8(void *stream, int32_t B, int32_t C, int32_t H, int32_t W, const uint8_t *d_img,
                    float *d_out, int64_t ld_out);
+/* DLogistic.log_prob (distlib.py:40-55) and IDFlows.log_likelihood's reduction
+ * (flows.py:154-169): x, mean, logscale hold n_groups contiguous groups of group_len
+ * symbols (one level of one image each).  Writes the per-symbol log-probability to d_logp
+ * (may be NULL) and each group's sum, in a fixed order, to d_group_sum (f64; may be NULL).
+ * Per symbol, in the reference's fp32 order: scale = exp(logscale),
+ * x+- = ((x +- 0.5/2^nbits) - mean)/scale, lp/ln = logsigmoid(x+-),
+ * logP = lp + log((1 - exp(ln - lp)) + eps). */
+int idf_log_prob(void *stream, int64_t n_groups, int64_t group_len, const float *d_x,
+                 const float *d_mean, const float *d_logscale, int32_t nbits, float eps,
+                 float *d_logp, double *d_group_sum);
 /* inverse of idf_dequant_u8 (exact on the grid); returns via d_bad[0] the count of
  * off-grid values (0 for a lossless decode). */
 int idf_quant_u8(void *stream, int32_t B, int32_t C, int32_t H, int32_t W, const float *d_in,

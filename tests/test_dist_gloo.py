@@ -119,3 +119,150 @@ def test_gather_residual_two_ranks(tmp_path):
         for rnk in range(2):
             for b in range(3):
                 assert r["st"][l * 6 + rnk * 3 + b] == parts[rnk][0][l * 3 + b]
+
+
+N_SYM = 131
+
+
+def _stream_inputs(l, b):
+    """Deterministic (x, mean, scale) of global stream (level l, image b)."""
+    import numpy as np
+    g = np.random.default_rng(1000 * l + b)
+    mean = g.integers(-64, 64, N_SYM).astype(np.float32) / 256
+    scale = np.exp(g.normal(-3, 1, N_SYM)).astype(np.float32)
+    x = (np.round((mean + scale * g.normal(0, 1, N_SYM)) * 256) / 256).astype(np.float32)
+    return x, mean, scale
+
+
+def _encode(pairs):
+    """oracle-encode the streams `pairs` [(l, b)] in order -> (states, nwords, words) torch."""
+    import sys
+    sys.path.insert(0, ORACLE)
+    import numpy as np
+    import rans_oracle
+    ins = [_stream_inputs(l, b) for l, b in pairs]
+    off = np.arange(len(pairs) + 1, dtype=np.int64) * N_SYM
+    cat = lambda i: np.concatenate([t[i] for t in ins]) if ins else np.zeros(0, np.float32)  # noqa
+    fs, words, nw, st = rans_oracle.encode_streams(off, cat(0), cat(1), cat(2))
+    w = np.concatenate([words[off[k]:off[k] + nw[k]] for k in range(len(pairs))] or
+                       [np.zeros(0, np.uint32)])
+    return (torch.from_numpy(fs.view(np.int64).copy()), torch.from_numpy(nw.astype(np.int64)),
+            torch.from_numpy(w.view(np.int32).copy()))
+
+
+def _scatter_worker(rank, world, port, n_images, out):
+    """rank 0 holds the single-batch bitstream; scatter -> every rank decodes its shard with
+    the oracle (exact symbols, final state 2^32) -> re-encodes it -> gather back to rank 0."""
+    import sys
+    sys.path.insert(0, PKG)
+    sys.path.insert(0, ORACLE)
+    import numpy as np
+    import rans_oracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from idfcodec.codec import Bitstream
+    from idfcodec.dist import (gather_bitstream, gather_streams, interleave_levels,
+                               scatter_bitstream, shard_range)
+    L = 2
+    shapes = [(1, 1, N_SYM)] * L
+    full = None
+    if rank == 0:
+        st, nw, w = _encode([(l, b) for l in range(L) for b in range(n_images)])
+        full = Bitstream(n_images, shapes, st, nw, w, None,
+                         {"n_subpixels": n_images * 10, "conv": "x3"})
+    mine, (lo, hi) = scatter_bitstream(full, src=0)
+    assert (lo, hi) == shard_range(n_images, rank, world)
+    assert mine.n_images == hi - lo and mine.meta["conv"] == "x3"
+    assert mine.meta["n_subpixels"] == (hi - lo) * 10 and mine.level_shapes == shapes
+    # decode every stream of the shard with the oracle
+    pairs = [(l, b) for l in range(L) for b in range(lo, hi)]
+    ns = len(pairs)
+    wnp = mine.words.numpy().view(np.uint32)
+    nwn = mine.nwords.numpy()
+    woff = np.concatenate([[0], np.cumsum(nwn)[:-1]]).astype(np.int64) if ns else np.zeros(0, np.int64)
+    off = np.arange(ns + 1, dtype=np.int64) * N_SYM
+    ins = [_stream_inputs(l, b) for l, b in pairs]
+    if ns:
+        fs, xs, stt = rans_oracle.decode_streams(
+            off, woff, nwn, wnp if wnp.size else np.zeros(1, np.uint32),
+            np.concatenate([t[1] for t in ins]), np.concatenate([t[2] for t in ins]),
+            mine.states.numpy().view(np.uint64))
+        assert (fs == 1 << 32).all() and (stt == 0).all()
+        assert np.array_equal(xs, np.concatenate([t[0] for t in ins]))
+    # encode the shard again and gather it back
+    st, nw, w = _encode(pairs)
+    got = gather_streams(st, nw, w, dst=0)
+    if n_images % world == 0:
+        local = Bitstream(hi - lo, shapes, st, nw, w, None,
+                          {"n_subpixels": (hi - lo) * 10, "conv": "x3"})
+        whole = gather_bitstream(local, dst=0)
+    if rank == 0:
+        counts = [shard_range(n_images, r, world)[1] - shard_range(n_images, r, world)[0]
+                  for r in range(world)]
+        st2, nw2, w2 = interleave_levels(*got, world, L, counts)
+        res = {"st": st2, "nw": nw2, "w": w2, "st0": full.states, "nw0": full.nwords,
+               "w0": full.words}
+        if n_images % world == 0:
+            res.update(ws=whole.states, wnw=whole.nwords, ww=whole.words,
+                       wn=torch.tensor(whole.n_images), wsub=torch.tensor(whole.meta["n_subpixels"]))
+        torch.save(res, out)
+    else:
+        assert got is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_images", [(2, 6), (2, 5), (3, 7)])
+def test_scatter_decode_gather_round_trip(tmp_path, world, n_images):
+    """Decode side of 8(e): scatter the single-batch bitstream, decode every shard, re-encode,
+    gather: the reassembled bitstream equals the original bit for bit (equal and ragged
+    shards)."""
+    out = str(tmp_path / "s.pt")
+    mp.spawn(_scatter_worker, args=(world, _free_port(), n_images, out), nprocs=world, join=True)
+    r = torch.load(out, weights_only=True)
+    assert torch.equal(r["st"], r["st0"]) and torch.equal(r["nw"], r["nw0"].to(torch.int64))
+    assert torch.equal(r["w"], r["w0"])
+    if "ws" in r:
+        assert torch.equal(r["ws"], r["st0"]) and torch.equal(r["ww"], r["w0"])
+        assert int(r["wn"]) == n_images and int(r["wsub"]) == n_images * 10
+
+
+def _bcast_worker(rank, world, port, out):
+    import sys
+    sys.path.insert(0, PKG)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from idfcodec.dist import broadcast_state
+    torch.manual_seed(rank)  # every rank starts from different weights
+    m = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.BatchNorm2d(8))
+    broadcast_state(m)
+    torch.save({k: v for k, v in m.state_dict().items()}, out + f".{rank}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_broadcast_state_two_ranks(tmp_path):
+    out = str(tmp_path / "b.pt")
+    mp.spawn(_bcast_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    a = torch.load(out + ".0", weights_only=True)
+    b = torch.load(out + ".1", weights_only=True)
+    torch.manual_seed(0)
+    ref = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.BatchNorm2d(8)).state_dict()
+    for k in ref:
+        assert torch.equal(a[k], b[k]) and torch.equal(a[k], ref[k]), k
+
+
+def test_bench_launches_n_ranks():
+    """`bench.py --gpus 2` starts 2 ranks itself (torch.distributed.run) without touching the
+    GPU in the parent; --launch-probe makes each rank report and exit."""
+    import json
+    import subprocess
+    import sys
+    from conftest import REPO
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2",
+                        "--launch-probe"], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert sorted(d["rank"] for d in lines) == [0, 1]
+    assert all(d["world"] == 2 for d in lines)

@@ -314,9 +314,58 @@ def test_bitstream_conv_flag_round_trips():
     st = torch.tensor([1 << 32, 5], dtype=torch.int64)
     nw = torch.tensor([1, 2], dtype=torch.int64)
     w = torch.tensor([7, 8, 9], dtype=torch.int32)
-    for mode in ("x3", "f32"):
+    for mode in ("x3", "f32", "halo", "gemm", "unfold", "bf16"):
         bs = Bitstream(1, [(6, 4, 4), (12, 2, 2)], st, nw, w, meta={"n_subpixels": 48, "conv": mode})
         back = Bitstream.from_bytes(bs.to_bytes())
         assert back.meta["conv"] == mode
     legacy = Bitstream(1, [(6, 4, 4), (12, 2, 2)], st, nw, w)  # written before the flag
     assert Bitstream.from_bytes(legacy.to_bytes()).meta["conv"] == "f32"
+
+
+def _codec_for(levels, family="x3", wx3=True):
+    from types import SimpleNamespace
+    from idfcodec.codec import ImageCodec
+    c = ImageCodec.__new__(ImageCodec)
+    c.engine = SimpleNamespace(levels=[SimpleNamespace(z=z, h=h, w=w) for z, h, w in levels],
+                               conv_family=family, wx3=wx3)
+    return c
+
+
+def test_decode_rejects_mismatched_container():
+    """A truncated, corrupted or other-config container raises before any device launch
+    (the rANS decode indexes streams by (level, image): no out-of-bounds reads)."""
+    import pytest
+    import torch
+    from idfcodec.codec import Bitstream
+    shapes = [(6, 4, 4), (12, 2, 2)]
+    c = _codec_for(shapes)
+
+    def bs(n_img=2, ns=4, nwords=None, nw_total=None, sh=shapes, conv="x3"):
+        nw = torch.tensor(nwords if nwords is not None else [1] * ns, dtype=torch.int64)
+        tot = int(nw.sum()) if nw_total is None else nw_total
+        return Bitstream(n_img, sh, torch.zeros(ns, dtype=torch.int64), nw,
+                         torch.zeros(tot, dtype=torch.int32), meta={"conv": conv})
+    c.check_bitstream(bs())  # well-formed
+    c.check_bitstream(bs(conv="f32"))  # switchable mode
+    with pytest.raises(ValueError, match="level shapes"):
+        c.check_bitstream(bs(sh=[(6, 4, 4), (12, 4, 4)]))
+    with pytest.raises(ValueError, match="level shapes"):
+        c.check_bitstream(bs(sh=shapes[:1], ns=2))
+    with pytest.raises(ValueError, match="streams"):
+        c.check_bitstream(bs(ns=3))
+    with pytest.raises(ValueError, match="negative"):
+        c.check_bitstream(bs(nwords=[1, -1, 1, 1]))
+    with pytest.raises(ValueError, match="word table"):
+        c.check_bitstream(bs(nw_total=2))
+    with pytest.raises(ValueError, match="coded with 'bf16'"):
+        c.check_bitstream(bs(conv="bf16"))
+    with pytest.raises(ValueError, match="coded with 'x3'"):
+        _codec_for(shapes, family="f32", wx3=False).check_bitstream(bs())
+    # a truncated container does not parse
+    good = bs().to_bytes()
+    with pytest.raises(ValueError):
+        Bitstream.from_bytes(good[:-3])
+    bad = bytearray(good)
+    bad[6] = 0x3F  # unknown conv code in the flags
+    with pytest.raises(ValueError):
+        Bitstream.from_bytes(bytes(bad))

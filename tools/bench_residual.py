@@ -39,29 +39,21 @@ DEFAULT_BATCH = {"resflow-cond-imagenet64": 1024, "resflows_smallpatch_split": 8
                  "resflow-patches-vqvae": 32}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="resflow-cond-imagenet64")
-    ap.add_argument("--batch", type=int, default=None, help="images per GPU")
-    ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--precision", default=None, choices=[None, "f32", "bf16"])
-    a = ap.parse_args()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+def run(config: str, batch: int | None = None, steps: int = 2, warmup: int = 1,
+        precision: str | None = None) -> dict | None:
+    """One residual config's encode+decode throughput on this rank's GPU (the process group,
+    if any, already initialised).  Returns the result dict on rank 0, None elsewhere."""
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    dev = torch.device("cuda", torch.cuda.current_device())
     from idfcodec import configs, synthetic
     from idfcodec.dist import gather_residual
-    codec, fl, vq, (H, W) = synthetic.build_residual(a.config, device=f"cuda:{local}",
-                                                     precision=a.precision)
-    pb, pr = configs.PAD.get(a.config, (0, 0))
+    codec, fl, vq, (H, W) = synthetic.build_residual(config, device=dev, precision=precision)
+    pb, pr = configs.PAD.get(config, (0, 0))
     Hs, Ws = H - pb, W - pr
-    per = a.batch or DEFAULT_BATCH.get(a.config, 8)
+    per = batch or DEFAULT_BATCH.get(config, 8)
     full = synthetic.images(per * world, H=Hs, W=Ws, seed=2)
-    img = full[rank * per:(rank + 1) * per].cuda()
+    img = full[rank * per:(rank + 1) * per].to(dev)
 
     def sync():
         torch.cuda.synchronize()
@@ -79,12 +71,12 @@ def main():
         torch.cuda.synchronize()
         return t1 - t0, time.perf_counter() - t1
 
-    for _ in range(a.warmup):
+    for _ in range(warmup):
         out, info = codec.decode(codec.encode(img))
     sync()
     te = td = 0.0
     merged = None
-    for _ in range(a.steps):
+    for _ in range(steps):
         sync()
         t0 = time.perf_counter()
         rbs = codec.encode(img)
@@ -100,27 +92,50 @@ def main():
     exact = bool(torch.equal(out, img))
     t_idx, t_rec = vq_time()
     if world > 1:
-        t = torch.tensor([te, td, t_idx, t_rec, 0.0 if exact else 1.0], device="cuda")
+        t = torch.tensor([te, td, t_idx, t_rec, 0.0 if exact else 1.0], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         te, td, t_idx, t_rec = (float(v) for v in t[:4])
         exact = float(t[4]) == 0.0
+    res = None
     if rank == 0:
         bs = merged if merged is not None else rbs
         px = per * world * Hs * Ws
-        print(json.dumps({
-            "metric": f"encode+decode Mpixels/s ({a.config}, bit-exact round trip)",
-            "value": round(px * a.steps / (te + td) / 1e6, 4), "unit": "Mpx/s", "n_gpus": world,
+        res = {
+            "metric": f"encode+decode Mpixels/s ({config}, bit-exact round trip)",
+            "value": round(px * steps / (te + td) / 1e6, 4), "unit": "Mpx/s", "n_gpus": world,
             "batch_per_gpu": per, "image": [3, Hs, Ws], "coded_image": [3, H, W],
-            "steps": a.steps, "encode_ms": round(te / a.steps * 1e3, 2),
-            "decode_ms": round(td / a.steps * 1e3, 2),
+            "steps": steps, "encode_ms": round(te / steps * 1e3, 2),
+            "decode_ms": round(td / steps * 1e3, 2),
+            "encode_mpx_s": round(px * steps / te / 1e6, 4),
+            "decode_mpx_s": round(px * steps / td / 1e6, 4),
             "vq_indices_ms": round(t_idx * 1e3, 2), "vq_reconstruct_ms": round(t_rec * 1e3, 2),
             "bpp": round(3 * bs.bpd(), 4), "index_bits_share": round(
                 1 - bs.flow.bits() / bs.bits(), 4),
             "round_trip_exact": exact, "scaling": "weak",
             "dtype": ("bf16 flow convs (f32 accumulate), f32 heads/VQ-VAE/CDF"
                       if fl.engine().precision == "bf16" else "f32"),
-            "data": "synthetic uint8, seeded weights"}),
-            flush=True)
+            "data": "synthetic uint8, seeded weights"}
+    del codec, fl, vq, img, full
+    torch.cuda.empty_cache()
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="resflow-cond-imagenet64")
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU")
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--precision", default=None, choices=[None, "f32", "bf16"])
+    a = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    res = run(a.config, a.batch, a.steps, a.warmup, a.precision)
+    if res is not None:
+        print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
