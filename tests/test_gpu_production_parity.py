@@ -197,7 +197,7 @@ def test_config3_bf16_blocks_teacher_forced(cfg3, lvl):
         worst_fp32 = max(worst_fp32, scaled_err(out, FO.dense_block(x, sd, "", mod.depth,
                                                                         mod.act_name)))
     print(f"config 3 level {lvl}: whole-block distance from the fp32 oracle {worst_fp32:.2e}")
-    assert worst_fp32 <= 0.1
+    assert worst_fp32 <= 5e-3  # measured 5.2e-4 .. 8.4e-4 (bf16 operands through 12 layers)
 
 
 def _fill_ws(eng, ws, d, B):
@@ -256,8 +256,7 @@ def test_reference_imagenet64_whole_level_streams(golden):
                                          d[f"scale{l}"].reshape(-1))
         assert int(fs[0]) == int(d[f"enclevel{l}/state"])
         assert int(nw[0]) == int(d[f"enclevel{l}/nwords"])
-        assert int(words[: nw[0]].astype(np.uint64).sum() % (1 << 64)) == \
-            int(d[f"enclevel{l}/wordsum"])
+        assert sum(int(v) for v in words[: nw[0]]) % (1 << 64) == int(d[f"enclevel{l}/wordsum"])
 
 
 def test_log_likelihood_matches_reference(golden, in64):
