@@ -11,7 +11,7 @@ cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 run() {
   local name=$1; shift
   timeout -k 10 400 rocprofv3 --kernel-trace --pmc "$@" -d gpurun_out/pmc_bench/$name -o run \
-    --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline \
+    --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-residual \
     > gpurun_out/pmc_bench/$name.log 2>&1
   local rc=$?; echo "pmc $name rc=$rc"; [ $rc -eq 0 ] || exit $rc
   cp gpurun_out/pmc_bench/$name/run_counter_collection.csv gpurun_out/pmc_bench/$name.csv
