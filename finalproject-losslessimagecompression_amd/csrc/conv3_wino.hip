@@ -42,7 +42,8 @@
 // Timing-only ablations for tools/native/wino_ablate (never set in the library build):
 // bit 0 skips the per-slab DMA, bit 1 skips the halo LDS reads, bit 2 skips the MFMAs,
 // bit 3 skips the input transform, bit 4 the in-loop barrier, bit 5 the U loads, bit 6
-// makes every halo DMA piece read 1 KiB of contiguous (wrong) memory.
+// makes every halo DMA piece read 1 KiB of contiguous (wrong) memory, bit 8 (256) skips the
+// X3 f16 split.
 #ifndef IDF_WINO_ABLATE
 #define IDF_WINO_ABLATE 0
 #endif
@@ -69,7 +70,6 @@
 #ifndef IDF_X3_K32
 #define IDF_X3_K32 0
 #endif
-
 namespace idf {
 
 typedef float w4 __attribute__((ext_vector_type(4)));
@@ -228,6 +228,11 @@ struct WinoRole {
 
   // P = this lane's tile base in the stage (quad image + 4 * tile slot)
   __device__ __forceinline__ void fetch_p(const float* P, w4 (&dd)[6]) const {
+    if (IDF_WINO_ABLATE & 2) {
+#pragma unroll
+      for (int e = 0; e < 6; ++e) dd[e] = w4{(float)e, 1.f, 2.f, 3.f};
+      return;
+    }
 #pragma unroll
     for (int e = 0; e < 6; ++e) {
       if constexpr (TWC > 0) dd[e] = *(const w4*)(P + oc(e));
@@ -335,6 +340,13 @@ struct WinoRole {
   template <bool CHECK>
   __device__ __forceinline__ static void split_pair(const w4& v0, const w4& v1, h4 (&hl)[4],
                                                     float& gmax, bool valid) {
+    if (IDF_WINO_ABLATE & 256) {  // no split: the f32 bits reinterpreted
+      hl[0] = __builtin_bit_cast(h4, __builtin_shufflevector(v0, v0, 0, 1));
+      hl[1] = __builtin_bit_cast(h4, __builtin_shufflevector(v0, v0, 2, 3));
+      hl[2] = __builtin_bit_cast(h4, __builtin_shufflevector(v1, v1, 0, 1));
+      hl[3] = __builtin_bit_cast(h4, __builtin_shufflevector(v1, v1, 2, 3));
+      return;
+    }
     split_f16(v0, hl[0], hl[1]);
     split_f16(v1, hl[2], hl[3]);
     if constexpr (CHECK) {  // valid = false for the pipeline's overrun past the last slab
@@ -1223,6 +1235,10 @@ static int wino_launch(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
     case 2: IDF_WINO_LAUNCH(2, slots, x3, chk); break; \
     default: IDF_WINO_LAUNCH(3, slots, x3, chk); break; \
   }
+#ifdef IDF_WINO_ONE  // register-allocation experiments: one instantiation only
+  hipLaunchKernelGGL((conv3_wino_kernel<IDF_WINO_ONE, kWSlots, true, false, 0>), dim3((unsigned)blocks),
+                     dim3(kWThreads), 0, s, g);
+#else
   if (pl.big) {
     if (!x3) IDF_WINO_NF(kWSlotsBig, false, false)
     else if (check_in) IDF_WINO_NF(kWSlotsBig, true, true)
@@ -1242,6 +1258,7 @@ static int wino_launch(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
     else IDF_WINO_NF(kWSlots, true, false)
 #undef IDF_WX3_TW
   }
+#endif
 #undef IDF_WINO_NF
 #undef IDF_WINO_LAUNCH
   if (pl.ksplit > 1) {
