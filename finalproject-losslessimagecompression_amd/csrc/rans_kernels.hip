@@ -10,20 +10,21 @@
 //                     fully parallel, HBM-bound (12 B in, 8 B out per symbol).
 //   rans_encode_prep: the streamed encoder's pass 1: (start, freq), the window
 //                     flag and 1/freq per symbol, fully parallel.
-//   rans_encode     : pass 2 (rans.pyx:61-66), one lane per stream; the serial
-//                     state chain with an exact 64/24-bit division done by the
-//                     precomputed double reciprocal plus integer correction, its
-//                     symbol records loaded 8 ahead of the chain.
+//   rans_encode     : pass 2 (rans.pyx:61-66), ONE WAVE per stream: the state chain
+//                     on the scalar unit (readlane of coalesced 64-symbol record chunks,
+//                     magic-reciprocal quotient), words stored 64 at a time.
+//   rans_decode_prep: decode pass 1, fully parallel: the EXACT CDF at the last bin of
+//                     each of the 2048-bin window's 64 blocks, per symbol.
 //   rans_decode     : rans.pyx:69-110, ONE WAVE per stream.  The reference's
 //                     11-12 step binary search over the 2048-bin window is
-//                     replaced by ONE round of 64 exact CDF probes placed by a
-//                     cheap float round (exact_window), with a two-round exact
-//                     64-ary search (exact_search) whenever the window does not
-//                     provably bracket the answer.  The CDF is strictly increasing
-//                     in s for scale > 0 (part2 steps by 1, part1 is monotone:
-//                     glibc expf verified monotone on every float), so every
-//                     search returns the reference's s; scale <= 0 or NaN falls
-//                     back to the reference's serial binary search.
+//                     replaced by one integer ballot of mod against the 64 exact block
+//                     boundaries and ONE round of 33 exact CDF probes over the chosen
+//                     block (cdf_bin: branch-free, bit-identical to rans_cdf).  The CDF
+//                     is strictly increasing in s for scale > 0 (part2 steps by 1,
+//                     part1 is monotone: glibc expf verified monotone on every float),
+//                     so this is the reference's s; scales outside the fast range take
+//                     a two-round exact 64-ary search and scale <= 0 or NaN the
+//                     reference's serial binary search.
 //   gather_words    : compacts per-stream word runs into one contiguous buffer.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -33,20 +34,16 @@
 
 #pragma clang fp contract(off)
 
-// Timing-only decode variants for tools/native/rans_bench (never set in the library build):
-// 1 = always the two-round exact search, 2 = exact window without the hoisted divisions,
-// 3 = no search at all (fake symbol), 4 = approximate rounds only, 5 = count fallbacks.
-#ifndef IDF_DECODE_MODE
-#define IDF_DECODE_MODE 0
+// Timing-only instrumentation for tools/native/rans_bench (never set in the library build):
+// s_memtime stamps at six points of the decode chain for symbols 0..255 of stream 0.
+#ifndef IDF_DECODE_STAMPS
+#define IDF_DECODE_STAMPS 0
 #endif
-#if IDF_DECODE_MODE == 5
-__device__ unsigned long long g_decode_fallbacks;
-#endif
-#if IDF_DECODE_MODE == 6
+#if IDF_DECODE_STAMPS
 __device__ unsigned long long g_stamp[256][6];
-#define STAMP(j) do { if (blockIdx.x == 0 && g_sym < 256) g_stamp[g_sym][j] = __builtin_amdgcn_s_memtime(); } while (0)
+#define STAMP(j, sym) do { if (k == 0 && (sym) < 256) g_stamp[(sym)][j] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
-#define STAMP(j) do { } while (0)
+#define STAMP(j, sym) do { } while (0)
 #endif
 
 namespace idf {
@@ -307,17 +304,69 @@ __device__ __forceinline__ int rans_cdf_rs(float x, float mean, float scale, flo
   return part1 + part2;
 }
 
-// Fast float estimate of the CDF (not bit-exact): used only to place the exact probe
-// window.  part2 (= s - lower + 1) is exact; part1's error is a few units of M.
-__device__ __forceinline__ int approx_cdf(int q, int lower, float mean, float rscale) {
-  const float u = ((float)q * (1.0f / 256.0f) + 0.001953125f - mean) * rscale;
-  const float l = __frcp_rn(1.0f + __expf(-u));
-  return (int)rintf(l * 16775168.0f) + (q - lower + 1);
+// part1 = round((M - 2048) / (1 + expf(-u))) of rans.pyx:34 as a function of the float
+// logistic argument u alone, on a short dependent chain (the decoder's critical path):
+//   * glibc expf's table path without its special-case branches; where glibc leaves that
+//     path the result is fixed -- x = -u > 0x1.62e42ep6: expf = inf, 1/(1+inf) = 0, part1 = 0;
+//     x < -0x1.9fe368p6 (also -inf): expf = 0, part1 = M - 2048 = 16775168 -- and so is an
+//     infinite 1 + expf, so one select at the end replaces them all;
+//   * 1/y by v_rcp_f64, ONE Newton step and the quotient correction (the IEEE division
+//     hipcc emits takes two Newton steps, div_scale and div_fixup);
+//   * roundf(p) for p >= 0 as (int)((double)p + 0.5): the sum is exact in double and the
+//     conversion truncates.
+// Equal to part1_ref (the reference's arithmetic) on every non-NaN float u
+// (idf_rans_part1_selfcheck: all 2^32 bit patterns); u is never NaN here (scale > 0).
+__device__ __forceinline__ int part1_ref(float u, const uint64_t* tab) {
+  const double l = 1.0 / (1.0 + (double)expf_glibc(-u, tab));
+  return (int)round_f((float)(l * 16775168.0));
+}
+__device__ __forceinline__ int part1_fast(float u, const uint64_t* tab) {
+  const double InvLn2N = 0x1.71547652b82fep+0 * 32;
+  const double SHIFT = 0x1.8p+52;
+  const double C0 = 0x1.c6af84b912394p-5 / (32.0 * 32.0 * 32.0);
+  const double C1 = 0x1.ebfce50fac4f3p-3 / (32.0 * 32.0);
+  const double C2 = 0x1.62e42ff0c52d6p-1 / 32.0;
+  const float x = -u;
+  const bool zero = x > 0x1.62e42ep6f, full = x < -0x1.9fe368p6f;
+  const double xd = (double)x;
+  double kd = __builtin_fma(InvLn2N, xd, SHIFT);
+  const uint64_t ki = d2u(kd);
+  kd -= SHIFT;
+  const double r = __builtin_fma(InvLn2N, xd, -kd);
+  const double sc = u2d(tab[ki % 32] + (ki << 47));
+  const double z = __builtin_fma(C0, r, C1);
+  const double r2 = r * r;
+  double ey = __builtin_fma(C2, r, 1.0);
+  ey = __builtin_fma(z, r2, ey);
+  const double y = 1.0 + (double)(float)(ey * sc);
+  double rc = __builtin_amdgcn_rcp(y);
+  rc = __builtin_fma(rc, __builtin_fma(-y, rc, 1.0), rc);
+  const double l = __builtin_fma(__builtin_fma(-y, rc, 1.0), rc, rc);  // 1/y, correctly rounded
+  const float p = (float)(l * 16775168.0);
+  const int pn = (int)((double)p + 0.5);
+  const bool fixed = zero || full || __builtin_isinf(y);
+  return fixed ? (full ? 16775168 : 0) : pn;
+}
+// The exact CDF at bin q (x = q/256) for scale > 0 with fast_scale_ok(scale): rans_cdf_rs with
+// the integer-exact forms of its x terms -- part2 = round((x - lower_f) * 256) + 1 = q - lower + 1
+// (both operands are multiples of 2^-8: the f32 subtraction is exact), (double)x + 2^-9 =
+// (2q + 1) * 2^-9 (exact) -- and part1_fast.
+__device__ __forceinline__ int cdf_bin(int q, int lower, double mean_d, double scale_d, double rs,
+                                       const uint64_t* tab) {
+  const double t = (double)(2 * q + 1) * 0.001953125 - mean_d;
+  const float u = (float)div_unscaled(t, scale_d, rs);
+  return part1_fast(u, tab) + (q - lower + 1);
+}
+// the exact CDF at bin q for any scale != 0 (rans_cdf, or cdf_bin where it applies)
+__device__ __forceinline__ int cdf_any(int q, int lower, float mean, float scale, const uint64_t* tab) {
+  if (scale > 0.0f && fast_scale_ok(scale))
+    return cdf_bin(q, lower, (double)mean, (double)scale, rcp_refined((double)scale), tab);
+  return rans_cdf(sym_x(q), mean, scale, rans_lower_f(lower), tab);
 }
 
 // Exact two-round 64-ary search over the reference window (rans.pyx:96-104 result):
 // round 1: lane L probes the last bin of block L; round 2: 33 lanes probe the chosen
-// block and its left neighbour.
+// block and its left neighbour.  The slow path: scale > 0 outside fast_scale_ok.
 __device__ __forceinline__ void exact_search(uint64_t mod, int lower, float mi, float si, float lf,
                                              int lane, int* s_out, int* c_lo, int* c_hi,
                                              const uint64_t* tab) {
@@ -345,59 +394,38 @@ __device__ __forceinline__ void exact_search(uint64_t mod, int lower, float mi, 
   *c_hi = __builtin_amdgcn_readlane(cq, kk);
 }
 
-// Decode pass 1 (fully parallel, off the serial chain): for every symbol, the float
-// estimate of the CDF at the last bin of each of the window's 64 blocks of 32 bins.
-// btab[i * 64 + l] = approx_cdf(lower_i + 32 l + 31).
+// Decode pass 1 (fully parallel, off the serial chain): for every symbol the EXACT CDF at
+// the last bin of each of the window's 64 blocks of 32 bins,
+// btab[i * 64 + l] = CDF(lower_i + 32 l + 31) (scale <= 0: unused, 0).
 __global__ void __launch_bounds__(256) rans_decode_prep_kernel(int64_t n, const float* __restrict__ mean,
                                                                const float* __restrict__ scale,
                                                                int32_t* __restrict__ btab) {
+  __shared__ uint64_t tab[32];
+  if (threadIdx.x < 32) tab[threadIdx.x] = kExp2fTab[threadIdx.x];
+  __syncthreads();
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t i = g >> 6;
   const int l = (int)(g & 63);
   if (i >= n) return;
   const float mi = mean[i], si = scale[i];
   const int lower = rans_lower_int(mi);
-  btab[g] = approx_cdf(lower + 32 * l + 31, lower, mi, __builtin_amdgcn_rcpf(si));
-}
-
-// One exact round: the precomputed block estimates (ablk: this lane's block) locate the
-// transition's 32-bin block, then 64 lanes evaluate the exact CDF on q = ws .. ws+63
-// centred on it.  Returns false (caller runs exact_search) unless the window provably
-// brackets the reference's answer: the CDF is strictly increasing for scale > 0, so the
-// answer is the first q >= lower with cdf(q) > mod, or lower + 2048 if no q <= lower + 2047
-// has one.  rs = rcp_refined(scale) when fast_scale_ok(scale).
-__device__ __forceinline__ bool exact_window(uint64_t mod, int lower, float mi, float si, float lf,
-                                             double rs, int ablk, int lane, int* s_out, int* c_lo,
-                                             int* c_hi, const uint64_t* tab, int g_sym = 0) {
-  const int64_t md = (int64_t)mod;
-  STAMP(1);
-  const uint64_t ma = __ballot((int64_t)ablk > md);
-  const int blk = ma ? __ffsll((unsigned long long)ma) - 1 : 64;
-  STAMP(2);
-  int ws = lower + 32 * blk + 16 - 32;  // the window is centred on the block
-  if (ws < lower - 1) ws = lower - 1;
-  if (ws > lower + 2048 - 63) ws = lower + 2048 - 63;
-  const int q = ws + lane;
-  const int cq = (IDF_DECODE_MODE != 2 && fast_scale_ok(si))
-                     ? rans_cdf_rs(sym_x(q), mi, si, lf, tab, rs)
-                     : rans_cdf(sym_x(q), mi, si, lf, tab);
-  const bool set = q > lower + 2047 || (int64_t)cq > md;
-  const uint64_t m = __ballot(set);
-  STAMP(3);
-  if ((m & 1ull) && ws >= lower) return false;  // answer may lie left of the window
-  const uint64_t m1 = m & ~1ull;
-  if (m1 == 0) return false;                       // answer right of the window
-  const int k = __ffsll((unsigned long long)m1) - 1;
-  *s_out = ws + k;
-  *c_lo = __builtin_amdgcn_readlane(cq, k - 1);  // k is wave-uniform
-  *c_hi = __builtin_amdgcn_readlane(cq, k);
-  STAMP(4);
-  return true;
+  btab[g] = si > 0.0f ? cdf_any(lower + 32 * l + 31, lower, mi, si, tab) : 0;
 }
 
 // WAVES streams per block, one per wave: the waves never synchronise after the table
 // load, so packing them only concentrates the decode on fewer CUs (nstreams / WAVES), which
 // leaves the rest of the chip to a concurrent lane's convolutions (ImageCodec lanes).
+//
+// Per symbol (rans.pyx:84-109), for scale > 0 in the fast range:
+//   1. one integer ballot of mod against the 64 exact block boundaries (pass 1) gives the
+//      block b of the reference's answer: the first block whose last bin has CDF > mod, or
+//      b = 64 when none has (then s = lower + 2048, rans.pyx's loop exit);
+//   2. ONE exact round: lane j evaluates the CDF at q = lower + 32 b - 1 + j (lanes 1..32
+//      the block, lane 0 its left neighbour); the CDF is strictly increasing for scale > 0
+//      (part2 steps by one, part1 is monotone: glibc expf verified monotone on every float),
+//      so the first lane in 1..32 with CDF > mod (or q past the window) is s, and lanes k-1,
+//      k hold CDF(s - 1), CDF(s) -- no bracket checks and no second search.
+// Other scales take the reference's own searches (exact_search, ref_binary_search).
 template <int WAVES>
 __global__ void __launch_bounds__(64 * WAVES) rans_decode_kernel(
     int64_t nstreams, const int64_t* __restrict__ sym_off, const int64_t* __restrict__ word_off,
@@ -406,7 +434,7 @@ __global__ void __launch_bounds__(64 * WAVES) rans_decode_kernel(
     const uint64_t* __restrict__ init_state, uint64_t* __restrict__ final_state,
     float* __restrict__ out, int32_t* __restrict__ status, const int32_t* __restrict__ btab) {
   __shared__ uint64_t tab[32];
-  // block estimates, 2 windows per wave
+  // block boundaries, 2 windows per wave
   __shared__ __attribute__((aligned(16))) int32_t bt_all[WAVES][2][64 * 64];
   if (threadIdx.x < 32) tab[threadIdx.x] = kExp2fTab[threadIdx.x];
   __syncthreads();
@@ -422,7 +450,7 @@ __global__ void __launch_bounds__(64 * WAVES) rans_decode_kernel(
   int32_t flag = 0;
   // Nothing the chain needs waits on memory: symbols are decoded in windows of 64 whose
   // (mean, scale) and derived (lower, 1/scale) sit one per lane, computed in parallel
-  // while the previous window decodes; the window's block estimates are copied into LDS
+  // while the previous window decodes; the window's block boundaries are copied into LDS
   // by DMA one window ahead; words come from a 64-word register window read with a
   // uniform lane index; each lane keeps its symbol's output for one coalesced store per
   // window.
@@ -446,74 +474,143 @@ __global__ void __launch_bounds__(64 * WAVES) rans_decode_kernel(
                                        16, 0, 0);
     }
   };
-  int64_t wbase = pos;  // lane l of wwin holds w[wbase - 1 - l]
-  uint32_t wwin = (wbase - 1 - lane >= 0) ? w[wbase - 1 - lane] : 0u;
+  // Words: a 128-word register buffer (lane l of wA holds w[wb - 1 - l], of wB w[wb - 65 - l])
+  // loaded at the START of the previous window from that window's pos: a window consumes at
+  // most 64 words (one per symbol, rans.pyx:86-89), so the buffer covers the next window too
+  // and no word read ever waits on memory.
+  auto ld_words = [&](int64_t base, uint32_t& a, uint32_t& c) {
+    const int64_t i0 = base - 1 - lane, i1 = base - 65 - lane;
+    a = i0 >= 0 ? w[i0] : 0u;
+    c = i1 >= 0 ? w[i1] : 0u;
+  };
+  int64_t wb = pos, wnb = pos;
+  uint32_t wA, wB, wnA, wnB;
+  ld_words(wb, wA, wB);
+  wnA = wA;
+  wnB = wB;
+  // rans.pyx:86-89 (buffer read in reverse), branch-free on the scalar unit; running out of
+  // words flags the stream (the reference indexes past its buffer) and decoding goes on
+  // with garbage that the status marks
+  auto renorm = [&]() {
+    const bool need = __builtin_amdgcn_readfirstlane((int)(state >> 32)) == 0;
+    const int idx = (int)(wb - pos);
+    const uint32_t wa = (uint32_t)__builtin_amdgcn_readlane((int)wA, idx & 63);
+    const uint32_t wc = (uint32_t)__builtin_amdgcn_readlane((int)wB, idx & 63);
+    const uint32_t word = idx < 64 ? wa : wc;
+    flag |= (need && pos <= 0) ? IDF_STREAM_UNDERFLOW : 0;
+    state = need ? ((state << 32) | (uint64_t)word) : state;
+    pos -= need ? 1 : 0;
+  };
   float mcur, scur, mnxt = 0.0f, snxt = 1.0f;
   ld_params(0, mcur, scur);
-  asm volatile("" ::"v"(wwin), "v"(mcur), "v"(scur));
+  asm volatile("" ::"v"(wA), "v"(wB), "v"(mcur), "v"(scur));
   if (n > 0) ld_blk(0, 0);
   bool stop = false;
   int slot = 0;
   for (int64_t j0 = 0; j0 < n && !stop; j0 += 64, slot ^= 1) {
     const int cnt = n - j0 < 64 ? (int)(n - j0) : 64;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this window's estimates have landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // boundaries, parameters, words landed
+    wA = wnA;  // j0 = 0: the same buffer
+    wB = wnB;
+    wb = wnb;
     if (j0 + 64 < n) {
       ld_blk(j0 + 64, slot ^ 1);
       ld_params(j0 + 64, mnxt, snxt);
+      ld_words(pos, wnA, wnB);
+      wnb = pos;
     }
     // per-lane derived parameters of this window's symbols
     const int lower_l = rans_lower_int(mcur);  // rans.pyx:91
-    const float lf_l = rans_lower_f(lower_l);  // rans.pyx:93
-    const double rs_l = fast_scale_ok(scur) ? rcp_refined((double)scur) : 0.0;
+    const bool fast_l = scur > 0.0f && fast_scale_ok(scur);
+    const double rs_l = fast_l ? rcp_refined((double)scur) : 0.0;
     float outv = 0.0f;
     int done = 0;
-    {
+    int ablk = bt[slot][lane];
+    // Windows whose symbols all take the fast path run a straight-line loop: the state stays
+    // in SGPRs, the next symbol's parameters and block boundaries are fetched one symbol
+    // ahead, and the loop has no branch but its back-edge.
+    if (__ballot(lane < cnt && !fast_l) == 0) {
+      const uint64_t rsb_l = __builtin_bit_cast(uint64_t, rs_l);
+      const int rs_hi_l = (int)(rsb_l >> 32), rs_lo_l = (int)(uint32_t)rsb_l;
+      const int mi_l = __builtin_bit_cast(int, mcur), si_l = __builtin_bit_cast(int, scur);
+      int n_lower = __builtin_amdgcn_readlane(lower_l, 0);
+      int n_mi = __builtin_amdgcn_readlane(mi_l, 0), n_si = __builtin_amdgcn_readlane(si_l, 0);
+      int n_rh = __builtin_amdgcn_readlane(rs_hi_l, 0), n_rl = __builtin_amdgcn_readlane(rs_lo_l, 0);
       for (int t = 0; t < cnt; ++t) {
-        const int ablk = bt[slot][t * 64 + lane];
-        if (state < kRansL) {  // rans.pyx:86-89 (buffer read in reverse)
-          if (pos <= 0) {
-            flag |= IDF_STREAM_UNDERFLOW;
-            stop = true;
-            break;
-          }
-          if (wbase - pos >= 64) {  // refill the word window
-            wbase = pos;
-            wwin = (wbase - 1 - lane >= 0) ? w[wbase - 1 - lane] : 0u;
-            // wait for it here, so the readlanes below never wait on the block estimates
-            asm volatile("" ::"v"(wwin));
-          }
-          const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)wwin, (int)(wbase - pos));
-          --pos;
-          state = (state << 32) | (uint64_t)word;
-        }
-        const uint64_t mod = state & 0xffffffull;
-        { const int g_sym = (int)(j0 + t); (void)g_sym; STAMP(0); }
+        const int lower = n_lower;
+        const double mi = (double)__builtin_bit_cast(float, n_mi);
+        const double si = (double)__builtin_bit_cast(float, n_si);
+        const double rs = __builtin_bit_cast(double, ((uint64_t)(uint32_t)n_rh << 32) | (uint32_t)n_rl);
+        const int tn = t + 1 < cnt ? t + 1 : t;
+        n_lower = __builtin_amdgcn_readlane(lower_l, tn);
+        n_mi = __builtin_amdgcn_readlane(mi_l, tn);
+        n_si = __builtin_amdgcn_readlane(si_l, tn);
+        n_rh = __builtin_amdgcn_readlane(rs_hi_l, tn);
+        n_rl = __builtin_amdgcn_readlane(rs_lo_l, tn);
+        const int anxt = bt[slot][tn * 64 + lane];
+        STAMP(0, j0 + t);
+        renorm();
+        const int mod = (int)(state & 0xffffffull);
+        STAMP(1, j0 + t);
+        const uint64_t mb = __ballot(ablk > mod);
+        const int blk = mb ? __ffsll((unsigned long long)mb) - 1 : 64;
+        const int base = lower + 32 * blk - 1;
+        const int q = base + lane;
+        STAMP(2, j0 + t);
+        const int cq = cdf_bin(q, lower, mi, si, rs, tab);
+        STAMP(3, j0 + t);
+        // lane 0 (q = base) is never the answer: CDF(base) <= mod for blk > 0, and for blk = 0
+        // the reference's search starts at lower = base + 1
+        const uint64_t m2 = __ballot(cq > mod || q > lower + 2047) & ~1ull;
+        const int kk = __ffsll((unsigned long long)m2) - 1;  // 1..32
+        const int c_lo = __builtin_amdgcn_readlane(cq, kk - 1);
+        const int c_hi = __builtin_amdgcn_readlane(cq, kk);
+        STAMP(4, j0 + t);
+        flag |= (c_lo < 0 || c_hi - c_lo < 0) ? IDF_STREAM_NEG_CDF : 0;
+        state = (state >> 24) * (uint64_t)(int64_t)(c_hi - c_lo) + (state & 0xffffffull) -
+                (uint64_t)(int64_t)c_lo;  // rans.pyx:108
+        STAMP(5, j0 + t);
+        outv = lane == t ? (float)(base + kk) * 0.00390625f : outv;  // message.push_back(s / 256.)
+        ablk = anxt;
+      }
+      done = cnt;
+    } else {
+      for (int t = 0; t < cnt; ++t) {
+        ablk = bt[slot][t * 64 + lane];
+        renorm();
+        const int mod = (int)(state & 0xffffffull);
+        const int lower = __builtin_amdgcn_readlane(lower_l, t);
         const float mi = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mcur), t));
         const float si = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, scur), t));
-        const int lower = __builtin_amdgcn_readlane(lower_l, t);
-        const float lf = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lf_l), t));
-        const uint64_t rsb = __builtin_bit_cast(uint64_t, rs_l);
-        const double rs = __builtin_bit_cast(
-            double, ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(rsb >> 32), t) << 32) |
-                        (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rsb, t));
-        int sym;
-        int c_lo, c_hi;
-        if (!(si > 0.0f)) {
-          if (si == 0.0f) {
+        int sym, c_lo, c_hi;
+        if (si > 0.0f && fast_scale_ok(si)) {
+          const uint64_t rsb = __builtin_bit_cast(uint64_t, rs_l);
+          const double rs = __builtin_bit_cast(
+              double, ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(rsb >> 32), t) << 32) |
+                          (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rsb, t));
+          const uint64_t mb = __ballot(ablk > mod);
+          const int blk = mb ? __ffsll((unsigned long long)mb) - 1 : 64;
+          const int base = lower + 32 * blk - 1;
+          const int q = base + lane;
+          const int cq = cdf_bin(q, lower, (double)mi, (double)si, rs, tab);
+          const uint64_t m2 = __ballot(cq > mod || q > lower + 2047) & ~1ull;
+          const int kk = __ffsll((unsigned long long)m2) - 1;
+          sym = base + kk;
+          c_lo = __builtin_amdgcn_readlane(cq, kk - 1);
+          c_hi = __builtin_amdgcn_readlane(cq, kk);
+        } else {
+          const float lf = rans_lower_f(lower);
+          if (si > 0.0f) {
+            exact_search((uint64_t)mod, lower, mi, si, lf, lane, &sym, &c_lo, &c_hi, tab);
+          } else if (si == 0.0f) {
             flag |= IDF_STREAM_SCALE_ZERO;
             stop = true;
             break;
+          } else {
+            sym = ref_binary_search((uint64_t)mod, lower, mi, si, lf, &flag, tab);
+            c_lo = rans_cdf(sym_x(sym - 1), mi, si, lf, tab);
+            c_hi = rans_cdf(sym_x(sym), mi, si, lf, tab);
           }
-          sym = ref_binary_search(mod, lower, mi, si, lf, &flag, tab);
-          c_lo = rans_cdf(sym_x(sym - 1), mi, si, lf, tab);
-          c_hi = rans_cdf(sym_x(sym), mi, si, lf, tab);
-        } else if (IDF_DECODE_MODE == 1 ||
-                   !exact_window(mod, lower, mi, si, lf, rs, ablk, lane, &sym, &c_lo, &c_hi, tab,
-                                 (int)(j0 + t))) {
-#if IDF_DECODE_MODE == 5
-          if (lane == 0) atomicAdd(&g_decode_fallbacks, 1ull);
-#endif
-          exact_search(mod, lower, mi, si, lf, lane, &sym, &c_lo, &c_hi, tab);
         }
         if (c_lo < 0 || c_hi - c_lo < 0) flag |= IDF_STREAM_NEG_CDF;
         const uint64_t cdf_s = (uint64_t)(int64_t)c_lo;
@@ -521,7 +618,6 @@ __global__ void __launch_bounds__(64 * WAVES) rans_decode_kernel(
         state = (state >> 24) * freq_s + (state & 0xffffffull) - cdf_s;  // rans.pyx:108
         if (lane == t) outv = sym_x(sym);  // message.push_back(s / 256.)
         done = t + 1;
-        { const int g_sym = (int)(j0 + t); (void)g_sym; STAMP(5); }
       }
     }
     if (lane < done) out[b + n - 1 - j0 - lane] = outv;
@@ -530,7 +626,7 @@ __global__ void __launch_bounds__(64 * WAVES) rans_decode_kernel(
   }
   if (lane == 0) {
     final_state[k] = state;
-    status[k] = flag | (pos != 0 ? IDF_STREAM_WORDS_LEFT : 0);
+    status[k] = flag | (pos > 0 ? IDF_STREAM_WORDS_LEFT : 0);
   }
 }
 
@@ -570,7 +666,24 @@ __global__ void __launch_bounds__(256) expf_checksum_kernel(uint64_t lo, uint64_
   if ((threadIdx.x & 63) == 0) atomicAdd(acc, sum);
 }
 
-// Self-check of rans_cdf_rs against rans_cdf on pseudo-random (x, mean, scale): scale
+// part1_fast == part1_ref over a range of float bit patterns of u (NaN skipped)
+__global__ void __launch_bounds__(256) part1_selfcheck_kernel(uint64_t lo, uint64_t hi,
+                                                              unsigned long long* bad) {
+  __shared__ uint64_t tab[32];
+  if (threadIdx.x < 32) tab[threadIdx.x] = kExp2fTab[threadIdx.x];
+  __syncthreads();
+  unsigned long long cnt = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi; i += stride) {
+    const float u = u2f((uint32_t)i);
+    if (u != u) continue;
+    cnt += part1_fast(u, tab) != part1_ref(u, tab);
+  }
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_down(cnt, o);
+  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(bad, cnt);
+}
+
+// Self-check of rans_cdf_rs and cdf_bin against rans_cdf on pseudo-random (x, mean, scale): scale
 // log-uniform over the fast range, mean in +-2^12, x on the 1/256 grid within the
 // window around mean.  Counts mismatching CDF values.
 __global__ void __launch_bounds__(256) cdf_selfcheck_kernel(uint64_t n, uint64_t seed,
@@ -593,7 +706,8 @@ __global__ void __launch_bounds__(256) cdf_selfcheck_kernel(uint64_t n, uint64_t
     if (!fast_scale_ok(scale)) continue;
     const int a = rans_cdf(x, mean, scale, lf, tab);
     const int b = rans_cdf_rs(x, mean, scale, lf, tab, rcp_refined((double)scale));
-    cnt += (a != b);
+    const int c = cdf_bin(sidx, lower, (double)mean, (double)scale, rcp_refined((double)scale), tab);
+    cnt += (a != b) + (a != c);
   }
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_down(cnt, o);
   if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(bad, cnt);
@@ -692,6 +806,12 @@ int idf_expf_glibc(void* stream, int64_t n, const float* in, float* out) {
 
 int idf_rans_cdf_selfcheck(void* stream, uint64_t n, uint64_t seed, unsigned long long* bad) {
   hipLaunchKernelGGL(cdf_selfcheck_kernel, dim3(4096), dim3(256), 0, (hipStream_t)stream, n, seed,
+                     bad);
+  return idf_last_error();
+}
+
+int idf_rans_part1_selfcheck(void* stream, uint64_t lo, uint64_t hi, unsigned long long* bad) {
+  hipLaunchKernelGGL(part1_selfcheck_kernel, dim3(8192), dim3(256), 0, (hipStream_t)stream, lo, hi,
                      bad);
   return idf_last_error();
 }

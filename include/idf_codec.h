@@ -99,6 +99,10 @@ int idf_expf_checksum(void *stream, uint64_t lo, uint64_t hi, unsigned long long
 /* Decoder self-check: the decode window's CDF (divisions with a hoisted reciprocal)
  * against the plain CDF on n pseudo-random (x, mean, scale); adds mismatches to *d_bad. */
 int idf_rans_cdf_selfcheck(void *stream, uint64_t n, uint64_t seed, unsigned long long *d_bad);
+/* Device self-check of the decoder's short-chain part1 (the logistic term of the CDF as a
+ * function of the float logistic argument u) against the reference arithmetic: adds to
+ * *d_bad the number of non-NaN float bit patterns u in [lo, hi) whose results differ. */
+int idf_rans_part1_selfcheck(void *stream, uint64_t lo, uint64_t hi, unsigned long long *d_bad);
 
 /* ======================================================================== *
  * Flow operators (integer-discrete flow, fp32).  Activations are stored

@@ -211,3 +211,48 @@ def test_decode_window_cdf_matches_plain_cdf():
     bad = torch.zeros(1, dtype=torch.int64, device="cuda")
     check(lib().idf_rans_cdf_selfcheck(_lib.stream_ptr(), 1 << 26, 12345, ptr(bad)), "selfcheck")
     assert int(bad.item()) == 0
+
+
+def test_decode_slow_paths_match_oracle(oracle):
+    """Scales outside the fast range (two-round exact search) and negative scales (the
+    reference's serial binary search) mixed into streams with ordinary ones: final states,
+    symbols and status equal the C oracle's decode (rans.pyx:69-110) of the same state and
+    words.  Words and states are random (decode is a function of them whether or not an
+    encoder produced them)."""
+    g = np.random.default_rng(11)
+    lens = g.integers(1, 400, 64)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    n = int(off[-1])
+    mean = (g.integers(-512, 513, n) / 256).astype(np.float32)
+    scale = (np.exp(6 * g.random(n) - 5)).astype(np.float32)
+    kind = g.integers(0, 4, n)
+    scale[kind == 1] = np.float32(2.0 ** -62)
+    scale[kind == 2] = np.float32(2.0 ** 62)
+    scale[kind == 3] = -np.float32(2.0 ** 40) * (1 + g.random((kind == 3).sum())).astype(np.float32)
+    words = g.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    init = (g.integers(1 << 32, 1 << 62, lens.size, dtype=np.uint64)).astype(np.uint64)
+    nw = lens.astype(np.int64)
+    rfs, rout, rst = oracle.decode_streams(off, off[:-1], nw, words, mean, scale, init)
+    dfs, out, dst = _dec_streams(off, off[:-1], nw, words, mean, scale, init)
+    ok = rst == 0
+    assert ok.sum() >= lens.size // 2  # most streams decode without a reference error
+    for k in np.flatnonzero(ok):
+        a, e = off[k], off[k + 1]
+        assert dfs[k] == rfs[k], k
+        assert np.array_equal(out[a:e], rout[a:e]), k
+        assert (dst[k] & ~32) == 0, (k, dst[k])  # at most IDF_STREAM_WORDS_LEFT
+    hit = np.zeros(n, bool)
+    for k in np.flatnonzero(ok):
+        hit[off[k]:off[k + 1]] = True
+    for kd in (1, 2, 3):  # every slow path ran inside an oracle-checked stream
+        assert (hit & (kind == kd)).sum() > 100, kd
+
+
+def test_decoder_part1_short_chain_exhaustive():
+    """The decoder's short-chain logistic term == the reference arithmetic
+    (round((M - 2048) / (1 + expf(-u))), IEEE division) for every non-NaN float u."""
+    from idfcodec import _lib
+    from idfcodec._lib import check, lib, ptr
+    bad = torch.zeros(1, dtype=torch.int64, device="cuda")
+    check(lib().idf_rans_part1_selfcheck(_lib.stream_ptr(), 0, 1 << 32, ptr(bad)), "part1")
+    assert int(bad.item()) == 0
