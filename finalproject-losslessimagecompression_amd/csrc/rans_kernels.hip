@@ -39,6 +39,9 @@
 #ifndef IDF_DECODE_STAMPS
 #define IDF_DECODE_STAMPS 0
 #endif
+#ifndef IDF_DECODE_FAKE_CDF
+#define IDF_DECODE_FAKE_CDF 0
+#endif
 #if IDF_DECODE_STAMPS
 __device__ unsigned long long g_stamp[256][6];
 #define STAMP(j, sym) do { if (k == 0 && (sym) < 256) g_stamp[(sym)][j] = __builtin_amdgcn_s_memtime(); } while (0)
@@ -305,15 +308,15 @@ __device__ __forceinline__ int rans_cdf_rs(float x, float mean, float scale, flo
 }
 
 // part1 = round((M - 2048) / (1 + expf(-u))) of rans.pyx:34 as a function of the float
-// logistic argument u alone, on a short dependent chain (the decoder's critical path):
-//   * glibc expf's table path without its special-case branches; where glibc leaves that
-//     path the result is fixed -- x = -u > 0x1.62e42ep6: expf = inf, 1/(1+inf) = 0, part1 = 0;
-//     x < -0x1.9fe368p6 (also -inf): expf = 0, part1 = M - 2048 = 16775168 -- and so is an
-//     infinite 1 + expf, so one select at the end replaces them all;
+// logistic argument u alone, in few instructions (the decoder's serial chain is issue-bound:
+// one wave, one instruction per ~4 cycles):
+//   * glibc expf's table path on x = -u clamped to [-0x1.9fe368p6, 0x1.62e42ep6] (one
+//     v_med3): outside that range glibc returns 0 (below) or inf (above), and the clamp ends
+//     give the same part1 through the table path -- expf(lo) is below 2^-53, so 1 + expf
+//     rounds to 1 and part1 = M - 2048; expf(hi) is ~2^128, so part1 rounds to 0;
 //   * 1/y by v_rcp_f64, ONE Newton step and the quotient correction (the IEEE division
 //     hipcc emits takes two Newton steps, div_scale and div_fixup);
-//   * roundf(p) for p >= 0 as (int)((double)p + 0.5): the sum is exact in double and the
-//     conversion truncates.
+//   * roundf(p) for p >= 0 as v_cvt_rpi_i32_f32 (floor(p + 0.5) without rounding the sum).
 // Equal to part1_ref (the reference's arithmetic) on every non-NaN float u
 // (idf_rans_part1_selfcheck: all 2^32 bit patterns); u is never NaN here (scale > 0).
 __device__ __forceinline__ int part1_ref(float u, const uint64_t* tab) {
@@ -326,8 +329,7 @@ __device__ __forceinline__ int part1_fast(float u, const uint64_t* tab) {
   const double C0 = 0x1.c6af84b912394p-5 / (32.0 * 32.0 * 32.0);
   const double C1 = 0x1.ebfce50fac4f3p-3 / (32.0 * 32.0);
   const double C2 = 0x1.62e42ff0c52d6p-1 / 32.0;
-  const float x = -u;
-  const bool zero = x > 0x1.62e42ep6f, full = x < -0x1.9fe368p6f;
+  const float x = __builtin_amdgcn_fmed3f(-u, -0x1.9fe368p6f, 0x1.62e42ep6f);
   const double xd = (double)x;
   double kd = __builtin_fma(InvLn2N, xd, SHIFT);
   const uint64_t ki = d2u(kd);
@@ -343,17 +345,19 @@ __device__ __forceinline__ int part1_fast(float u, const uint64_t* tab) {
   rc = __builtin_fma(rc, __builtin_fma(-y, rc, 1.0), rc);
   const double l = __builtin_fma(__builtin_fma(-y, rc, 1.0), rc, rc);  // 1/y, correctly rounded
   const float p = (float)(l * 16775168.0);
-  const int pn = (int)((double)p + 0.5);
-  const bool fixed = zero || full || __builtin_isinf(y);
-  return fixed ? (full ? 16775168 : 0) : pn;
+  int pn;
+  asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(pn) : "v"(p));
+  return pn;
 }
 // The exact CDF at bin q (x = q/256) for scale > 0 with fast_scale_ok(scale): rans_cdf_rs with
 // the integer-exact forms of its x terms -- part2 = round((x - lower_f) * 256) + 1 = q - lower + 1
 // (both operands are multiples of 2^-8: the f32 subtraction is exact), (double)x + 2^-9 =
-// (2q + 1) * 2^-9 (exact) -- and part1_fast.
+// (2q + 1) * 2^-9 (exact, so fma((2q + 1), 2^-9, -mean) is the reference's rounded difference)
+// -- and part1_fast.
 __device__ __forceinline__ int cdf_bin(int q, int lower, double mean_d, double scale_d, double rs,
                                        const uint64_t* tab) {
-  const double t = (double)(2 * q + 1) * 0.001953125 - mean_d;
+  // (2q + 1) * 2^-9 is exact, so one fma rounds exactly as the reference's subtraction
+  const double t = __builtin_fma((double)(2 * q + 1), 0.001953125, -mean_d);
   const float u = (float)div_unscaled(t, scale_d, rs);
   return part1_fast(u, tab) + (q - lower + 1);
 }
@@ -394,12 +398,20 @@ __device__ __forceinline__ void exact_search(uint64_t mod, int lower, float mi, 
   *c_hi = __builtin_amdgcn_readlane(cq, kk);
 }
 
+// Per-symbol parameters of the decoder's fast loop, precomputed by pass 1 (32 B): the
+// window origin, -mean and scale widened to double and the refined reciprocal of the scale.
+struct DecRec {
+  int32_t lower, pad;
+  double mneg, sd, rs;
+};
+
 // Decode pass 1 (fully parallel, off the serial chain): for every symbol the EXACT CDF at
 // the last bin of each of the window's 64 blocks of 32 bins,
-// btab[i * 64 + l] = CDF(lower_i + 32 l + 31) (scale <= 0: unused, 0).
+// btab[i * 64 + l] = CDF(lower_i + 32 l + 31) (scale <= 0: unused, 0), and its DecRec.
 __global__ void __launch_bounds__(256) rans_decode_prep_kernel(int64_t n, const float* __restrict__ mean,
                                                                const float* __restrict__ scale,
-                                                               int32_t* __restrict__ btab) {
+                                                               int32_t* __restrict__ btab,
+                                                               DecRec* __restrict__ rec) {
   __shared__ uint64_t tab[32];
   if (threadIdx.x < 32) tab[threadIdx.x] = kExp2fTab[threadIdx.x];
   __syncthreads();
@@ -410,6 +422,10 @@ __global__ void __launch_bounds__(256) rans_decode_prep_kernel(int64_t n, const 
   const float mi = mean[i], si = scale[i];
   const int lower = rans_lower_int(mi);
   btab[g] = si > 0.0f ? cdf_any(lower + 32 * l + 31, lower, mi, si, tab) : 0;
+  if (l == 0) {
+    const bool fast = si > 0.0f && fast_scale_ok(si);
+    rec[i] = DecRec{lower, 0, -(double)mi, (double)si, fast ? rcp_refined((double)si) : 0.0};
+  }
 }
 
 // WAVES streams per block, one per wave: the waves never synchronise after the table
@@ -432,16 +448,19 @@ __global__ void __launch_bounds__(64 * WAVES) rans_decode_kernel(
     const int64_t* __restrict__ nwords, const uint32_t* __restrict__ words,
     const float* __restrict__ mean, const float* __restrict__ scale,
     const uint64_t* __restrict__ init_state, uint64_t* __restrict__ final_state,
-    float* __restrict__ out, int32_t* __restrict__ status, const int32_t* __restrict__ btab) {
+    float* __restrict__ out, int32_t* __restrict__ status, const int32_t* __restrict__ btab,
+    const DecRec* __restrict__ rec) {
   __shared__ uint64_t tab[32];
-  // block boundaries, 2 windows per wave
+  // block boundaries and parameter records, 2 windows per wave
   __shared__ __attribute__((aligned(16))) int32_t bt_all[WAVES][2][64 * 64];
+  __shared__ __attribute__((aligned(16))) DecRec rc_all[WAVES][2][64];
   if (threadIdx.x < 32) tab[threadIdx.x] = kExp2fTab[threadIdx.x];
   __syncthreads();
   const int wave = WAVES == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t k = (int64_t)blockIdx.x * WAVES + wave;
   if (k >= nstreams) return;
   auto& bt = bt_all[wave];
+  auto& rc = rc_all[wave];
   const int lane = threadIdx.x & 63;
   const int64_t b = sym_off[k], n = sym_off[k + 1] - b;
   const uint32_t* w = words + word_off[k];
@@ -463,9 +482,17 @@ __global__ void __launch_bounds__(64 * WAVES) rans_decode_kernel(
       sv = scale[i];
     }
   };
-  // window at j0 -> bt[slot][t * 64 + l] = btab[(i_hi - t) * 64 + l], i_hi = b + n - 1 - j0
+  // window at j0 -> bt[slot][t * 64 + l] = btab[(i_hi - t) * 64 + l], i_hi = b + n - 1 - j0,
+  // rc[slot][t] = rec[i_hi - t]
   auto ld_blk = [&](int64_t j0, int slot) {
     const int cnt = n - j0 < 64 ? (int)(n - j0) : 64;
+    for (int m = 0; m < 2; ++m) {  // 32 records (1 KiB) per DMA wave-instruction, 2 lanes each
+      const int tl = 32 * m + (lane >> 1);
+      const int64_t i = b + n - 1 - j0 - (tl < cnt ? tl : cnt - 1);
+      __builtin_amdgcn_global_load_lds((const void*)((const char*)(rec + i) + 16 * (lane & 1)),
+                                       (__attribute__((address_space(3))) void*)(&rc[slot][32 * m]),
+                                       16, 0, 0);
+    }
     for (int t = 0; t < cnt; t += 4) {  // 4 symbols (1 KiB) per DMA wave-instruction
       const int tl = t + (lane >> 4);
       const int64_t i = b + n - 1 - j0 - (tl < cnt ? tl : cnt - 1);
@@ -501,6 +528,13 @@ __global__ void __launch_bounds__(64 * WAVES) rans_decode_kernel(
     state = need ? ((state << 32) | (uint64_t)word) : state;
     pos -= need ? 1 : 0;
   };
+  // the word a renormalisation at the current pos would read (w[pos - 1])
+  auto next_word = [&]() -> uint32_t {
+    const int idx = (int)(wb - pos);
+    const uint32_t wa = (uint32_t)__builtin_amdgcn_readlane((int)wA, idx & 63);
+    const uint32_t wc = (uint32_t)__builtin_amdgcn_readlane((int)wB, idx & 63);
+    return idx < 64 ? wa : wc;
+  };
   float mcur, scur, mnxt = 0.0f, snxt = 1.0f;
   ld_params(0, mcur, scur);
   asm volatile("" ::"v"(wA), "v"(wB), "v"(mcur), "v"(scur));
@@ -530,49 +564,64 @@ __global__ void __launch_bounds__(64 * WAVES) rans_decode_kernel(
     // in SGPRs, the next symbol's parameters and block boundaries are fetched one symbol
     // ahead, and the loop has no branch but its back-edge.
     if (__ballot(lane < cnt && !fast_l) == 0) {
-      const uint64_t rsb_l = __builtin_bit_cast(uint64_t, rs_l);
-      const int rs_hi_l = (int)(rsb_l >> 32), rs_lo_l = (int)(uint32_t)rsb_l;
-      const int mi_l = __builtin_bit_cast(int, mcur), si_l = __builtin_bit_cast(int, scur);
-      int n_lower = __builtin_amdgcn_readlane(lower_l, 0);
-      int n_mi = __builtin_amdgcn_readlane(mi_l, 0), n_si = __builtin_amdgcn_readlane(si_l, 0);
-      int n_rh = __builtin_amdgcn_readlane(rs_hi_l, 0), n_rl = __builtin_amdgcn_readlane(rs_lo_l, 0);
+      // The window's words in ONE register: lane l holds w[P - 1 - l], P = pos now (a window
+      // reads at most 64 words), gathered from the 128-word buffer.
+      const int P = (int)pos;
+      const int dsh = (int)(wb - pos);  // 0..64
+      const int src = ((lane + dsh) & 63) * 4;
+      const uint32_t ga = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)wA);
+      const uint32_t gc = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)wB);
+      const uint32_t wcur = lane + dsh < 64 ? ga : gc;
+      int ipos = P;
+      uint32_t wnext = (uint32_t)__builtin_amdgcn_readlane((int)wcur, 0);
+      int outi = 0;  // lane t: s - lower of symbol t
       for (int t = 0; t < cnt; ++t) {
-        const int lower = n_lower;
-        const double mi = (double)__builtin_bit_cast(float, n_mi);
-        const double si = (double)__builtin_bit_cast(float, n_si);
-        const double rs = __builtin_bit_cast(double, ((uint64_t)(uint32_t)n_rh << 32) | (uint32_t)n_rl);
-        const int tn = t + 1 < cnt ? t + 1 : t;
-        n_lower = __builtin_amdgcn_readlane(lower_l, tn);
-        n_mi = __builtin_amdgcn_readlane(mi_l, tn);
-        n_si = __builtin_amdgcn_readlane(si_l, tn);
-        n_rh = __builtin_amdgcn_readlane(rs_hi_l, tn);
-        n_rl = __builtin_amdgcn_readlane(rs_lo_l, tn);
-        const int anxt = bt[slot][tn * 64 + lane];
+        const DecRec R = rc[slot][t];  // uniform LDS reads
+        const int ab = bt[slot][t * 64 + lane];
         STAMP(0, j0 + t);
-        renorm();
+        {  // rans.pyx:86-89 with the next word already in an SGPR: compare and select only
+          uint32_t need;
+          asm volatile("s_cmp_eq_u32 %1, 0\n\ts_cselect_b32 %0, 1, 0"
+                       : "=s"(need) : "s"((uint32_t)(state >> 32)) : "scc");
+          state = need ? ((state << 32) | (uint64_t)wnext) : state;
+          ipos -= (int)need;
+        }
         const int mod = (int)(state & 0xffffffull);
         STAMP(1, j0 + t);
-        const uint64_t mb = __ballot(ablk > mod);
-        const int blk = mb ? __ffsll((unsigned long long)mb) - 1 : 64;
-        const int base = lower + 32 * blk - 1;
-        const int q = base + lane;
+        const uint64_t mb = __ballot(ab > mod);
+        uint32_t blk;  // first block whose last bin has CDF > mod, 64 if none (s_ff1 of 0 is -1)
+        asm volatile("s_ff1_i32_b64 %0, %1\n\ts_min_u32 %0, %0, 64" : "=&s"(blk) : "s"(mb) : "scc");
+        const int bs = 32 * (int)blk - 1;  // probe base - lower
+        const int q = R.lower + bs + lane;
         STAMP(2, j0 + t);
-        const int cq = cdf_bin(q, lower, mi, si, rs, tab);
+#if IDF_DECODE_FAKE_CDF  // timing-only: the loop skeleton without the CDF's dependent chain
+        const int cq = (lane << 19) + (int)(R.sd > R.rs);
+#else
+        const double td = __builtin_fma((double)(2 * q + 1), 0.001953125, R.mneg);
+        const float u = (float)div_unscaled(td, R.sd, R.rs);
+        const int cq = part1_fast(u, tab) + bs + 1 + lane;  // + part2 = q - lower + 1
+#endif
         STAMP(3, j0 + t);
         // lane 0 (q = base) is never the answer: CDF(base) <= mod for blk > 0, and for blk = 0
-        // the reference's search starts at lower = base + 1
-        const uint64_t m2 = __ballot(cq > mod || q > lower + 2047) & ~1ull;
-        const int kk = __ffsll((unsigned long long)m2) - 1;  // 1..32
+        // the reference's search starts at lower = base + 1; blk = 64: s = lower + 2048
+        const uint64_t m2 = __ballot(cq > mod) & ~1ull;
+        const int kk = mb ? (int)__builtin_ctzll(m2) : 1;  // 1..32
         const int c_lo = __builtin_amdgcn_readlane(cq, kk - 1);
         const int c_hi = __builtin_amdgcn_readlane(cq, kk);
         STAMP(4, j0 + t);
-        flag |= (c_lo < 0 || c_hi - c_lo < 0) ? IDF_STREAM_NEG_CDF : 0;
-        state = (state >> 24) * (uint64_t)(int64_t)(c_hi - c_lo) + (state & 0xffffffull) -
-                (uint64_t)(int64_t)c_lo;  // rans.pyx:108
+        // freq >= 1 and c_lo >= 0 here (part2 steps by one, part1 >= 0); mod - c_lo may be
+        // negative (blk = 0), the sum is the reference's modulo 2^64
+        state = (state >> 24) * (uint64_t)(uint32_t)(c_hi - c_lo) + (uint64_t)(int64_t)(mod - c_lo);
         STAMP(5, j0 + t);
-        outv = lane == t ? (float)(base + kk) * 0.00390625f : outv;  // message.push_back(s / 256.)
-        ablk = anxt;
+        {  // message.push_back(s / 256.): lane t keeps s - lower
+          const int sv = bs + kk;
+          asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(outi) : "s"(sv), "s"(t) : "m0");
+        }
+        wnext = (uint32_t)__builtin_amdgcn_readlane((int)wcur, (P - ipos) & 63);
       }
+      pos = ipos;
+      flag |= ipos < 0 ? IDF_STREAM_UNDERFLOW : 0;  // ran out of words (pos never grows)
+      outv = (float)(outi + lower_l) * 0.00390625f;
       done = cnt;
     } else {
       for (int t = 0; t < cnt; ++t) {
@@ -762,7 +811,7 @@ static int decode_waves_per_block() {
 }
 
 int64_t idf_rans_decode_workspace_bytes(int64_t nsym) {
-  return 64 * (int64_t)sizeof(int32_t) * (nsym > 0 ? nsym : 1);
+  return (64 * (int64_t)sizeof(int32_t) + (int64_t)sizeof(DecRec)) * (nsym > 0 ? nsym : 1);
 }
 
 int idf_rans_decode_streams(void* stream, int64_t nstreams, int64_t nsym, const int64_t* sym_off,
@@ -774,17 +823,18 @@ int idf_rans_decode_streams(void* stream, int64_t nstreams, int64_t nsym, const 
   if (nstreams == 0) return IDF_OK;
   if (workspace_bytes < idf_rans_decode_workspace_bytes(nsym)) return IDF_ERR_WORKSPACE;
   int32_t* btab = (int32_t*)workspace;
+  DecRec* rec = (DecRec*)(btab + 64 * (nsym > 0 ? nsym : 1));
   if (nsym > 0)
     hipLaunchKernelGGL(rans_decode_prep_kernel, dim3((unsigned)((nsym * 64 + 255) / 256)), dim3(256),
-                       0, (hipStream_t)stream, nsym, mean, scale, btab);
+                       0, (hipStream_t)stream, nsym, mean, scale, btab, rec);
   if (decode_waves_per_block() == 4)
     hipLaunchKernelGGL(rans_decode_kernel<4>, dim3((unsigned)((nstreams + 3) / 4)), dim3(256), 0,
                        (hipStream_t)stream, nstreams, sym_off, word_off, nwords, words, mean,
-                       scale, init_state, final_state, out, status, btab);
+                       scale, init_state, final_state, out, status, btab, rec);
   else
     hipLaunchKernelGGL(rans_decode_kernel<1>, dim3((unsigned)nstreams), dim3(64), 0,
                        (hipStream_t)stream, nstreams, sym_off, word_off, nwords, words, mean,
-                       scale, init_state, final_state, out, status, btab);
+                       scale, init_state, final_state, out, status, btab, rec);
   return idf_last_error();
 }
 
