@@ -398,10 +398,11 @@ __device__ __forceinline__ void exact_search(uint64_t mod, int lower, float mi, 
   *c_hi = __builtin_amdgcn_readlane(cq, kk);
 }
 
-// Per-symbol parameters of the decoder's fast loop, precomputed by pass 1 (32 B): the
-// window origin, -mean and scale widened to double and the refined reciprocal of the scale.
+// Per-symbol parameters of the decoder's fast loop, precomputed by pass 1 (32 B): twice the
+// window origin plus one, -mean and scale widened to double and the refined reciprocal of the
+// scale.
 struct DecRec {
-  int32_t lower, pad;
+  int32_t l2, pad;  // 2 * lower + 1
   double mneg, sd, rs;
 };
 
@@ -424,7 +425,7 @@ __global__ void __launch_bounds__(256) rans_decode_prep_kernel(int64_t n, const 
   btab[g] = si > 0.0f ? cdf_any(lower + 32 * l + 31, lower, mi, si, tab) : 0;
   if (l == 0) {
     const bool fast = si > 0.0f && fast_scale_ok(si);
-    rec[i] = DecRec{lower, 0, -(double)mi, (double)si, fast ? rcp_refined((double)si) : 0.0};
+    rec[i] = DecRec{2 * lower + 1, 0, -(double)mi, (double)si, fast ? rcp_refined((double)si) : 0.0};
   }
 }
 
@@ -452,8 +453,9 @@ __global__ void __launch_bounds__(64 * WAVES) rans_decode_kernel(
     const DecRec* __restrict__ rec) {
   __shared__ uint64_t tab[32];
   // block boundaries and parameter records, 2 windows per wave
-  __shared__ __attribute__((aligned(16))) int32_t bt_all[WAVES][2][64 * 64];
-  __shared__ __attribute__((aligned(16))) DecRec rc_all[WAVES][2][64];
+  // (one spare row each: the fast loop reads one symbol ahead unconditionally)
+  __shared__ __attribute__((aligned(16))) int32_t bt_all[WAVES][2][65 * 64];
+  __shared__ __attribute__((aligned(16))) DecRec rc_all[WAVES][2][65];
   if (threadIdx.x < 32) tab[threadIdx.x] = kExp2fTab[threadIdx.x];
   __syncthreads();
   const int wave = WAVES == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -575,30 +577,44 @@ __global__ void __launch_bounds__(64 * WAVES) rans_decode_kernel(
       int ipos = P;
       uint32_t wnext = (uint32_t)__builtin_amdgcn_readlane((int)wcur, 0);
       int outi = 0;  // lane t: s - lower of symbol t
-      for (int t = 0; t < cnt; ++t) {
-        const DecRec R = rc[slot][t];  // uniform LDS reads
-        const int ab = bt[slot][t * 64 + lane];
+      uint32_t st_lo = (uint32_t)state, st_hi = (uint32_t)(state >> 32);
+      // LDS addresses kept in VGPRs (one add per symbol each, immediate offsets per field); the
+      // next symbol's record and block boundaries are read one symbol ahead
+      typedef int i4 __attribute__((ext_vector_type(4)));
+      typedef __attribute__((address_space(3))) const i4* lds_i4;
+      typedef __attribute__((address_space(3))) const int* lds_i1;
+      int ra = (int)(uintptr_t)(const __attribute__((address_space(3))) void*)&rc[slot][0];
+      int ba = (int)(uintptr_t)(const __attribute__((address_space(3))) void*)&bt[slot][lane];
+      asm volatile("" : "+v"(ra), "+v"(ba));
+      const int l2lane = 2 * lane;
+      // one symbol: record (r0, r1) and block boundaries ab were read one symbol ahead
+      auto symbol = [&](const i4& r0, const i4& r1, const int abc, const int t) {
+        const int L2 = r0[0];
+        const double mneg = __builtin_bit_cast(double, (uint64_t)(uint32_t)r0[2] | ((uint64_t)(uint32_t)r0[3] << 32));
+        const double sd = __builtin_bit_cast(double, (uint64_t)(uint32_t)r1[0] | ((uint64_t)(uint32_t)r1[1] << 32));
+        const double rs = __builtin_bit_cast(double, (uint64_t)(uint32_t)r1[2] | ((uint64_t)(uint32_t)r1[3] << 32));
         STAMP(0, j0 + t);
-        {  // rans.pyx:86-89 with the next word already in an SGPR: compare and select only
-          uint32_t need;
-          asm volatile("s_cmp_eq_u32 %1, 0\n\ts_cselect_b32 %0, 1, 0"
-                       : "=s"(need) : "s"((uint32_t)(state >> 32)) : "scc");
-          state = need ? ((state << 32) | (uint64_t)wnext) : state;
-          ipos -= (int)need;
-        }
-        const int mod = (int)(state & 0xffffffull);
+        // rans.pyx:86-89 with the next word already in an SGPR: SCC = (state < 2^32) selects
+        // the shifted state and borrows one from pos
+        asm volatile(
+            "s_cmp_eq_u32 %1, 0\n\t"
+            "s_cselect_b32 %1, %0, %1\n\t"
+            "s_cselect_b32 %0, %3, %0\n\t"
+            "s_subb_u32 %2, %2, 0"
+            : "+s"(st_lo), "+s"(st_hi), "+s"(ipos) : "s"(wnext) : "scc");
+        const int mod = (int)(st_lo & 0xffffffu);
         STAMP(1, j0 + t);
-        const uint64_t mb = __ballot(ab > mod);
+        const uint64_t mb = __ballot(abc > mod);
         uint32_t blk;  // first block whose last bin has CDF > mod, 64 if none (s_ff1 of 0 is -1)
         asm volatile("s_ff1_i32_b64 %0, %1\n\ts_min_u32 %0, %0, 64" : "=&s"(blk) : "s"(mb) : "scc");
         const int bs = 32 * (int)blk - 1;  // probe base - lower
-        const int q = R.lower + bs + lane;
         STAMP(2, j0 + t);
 #if IDF_DECODE_FAKE_CDF  // timing-only: the loop skeleton without the CDF's dependent chain
-        const int cq = (lane << 19) + (int)(R.sd > R.rs);
+        const int cq = (lane << 19) + (int)(sd > rs) + (int)(mneg > 0.0) + L2;
 #else
-        const double td = __builtin_fma((double)(2 * q + 1), 0.001953125, R.mneg);
-        const float u = (float)div_unscaled(td, R.sd, R.rs);
+        // q = lower + bs + lane: 2q + 1 = L2 + 2 bs + 2 lane
+        const double td = __builtin_fma((double)(L2 + 2 * bs + l2lane), 0.001953125, mneg);
+        const float u = (float)div_unscaled(td, sd, rs);
         const int cq = part1_fast(u, tab) + bs + 1 + lane;  // + part2 = q - lower + 1
 #endif
         STAMP(3, j0 + t);
@@ -611,14 +627,35 @@ __global__ void __launch_bounds__(64 * WAVES) rans_decode_kernel(
         STAMP(4, j0 + t);
         // freq >= 1 and c_lo >= 0 here (part2 steps by one, part1 >= 0); mod - c_lo may be
         // negative (blk = 0), the sum is the reference's modulo 2^64
-        state = (state >> 24) * (uint64_t)(uint32_t)(c_hi - c_lo) + (uint64_t)(int64_t)(mod - c_lo);
+        const uint64_t st = (((uint64_t)st_hi << 32 | st_lo) >> 24) * (uint64_t)(uint32_t)(c_hi - c_lo) +
+                            (uint64_t)(int64_t)(mod - c_lo);
+        st_lo = (uint32_t)st;
+        st_hi = (uint32_t)(st >> 32);
         STAMP(5, j0 + t);
         {  // message.push_back(s / 256.): lane t keeps s - lower
           const int sv = bs + kk;
           asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(outi) : "s"(sv), "s"(t) : "m0");
         }
         wnext = (uint32_t)__builtin_amdgcn_readlane((int)wcur, (P - ipos) & 63);
+      };
+      // two register sets, so the one-ahead reads need no copies; reads past the window's
+      // last symbol land in the spare row and are never used
+      i4 a0 = *(lds_i4)(uintptr_t)ra, a1 = *(lds_i4)(uintptr_t)(ra + 16);
+      int aab = *(lds_i1)(uintptr_t)ba;
+      int t = 0;
+      for (; t + 1 < cnt; t += 2) {
+        const i4 b0 = *(lds_i4)(uintptr_t)(ra + 32), b1 = *(lds_i4)(uintptr_t)(ra + 48);
+        const int bab = *(lds_i1)(uintptr_t)(ba + 256);
+        symbol(a0, a1, aab, t);
+        ra += 64;
+        ba += 512;
+        a0 = *(lds_i4)(uintptr_t)ra;
+        a1 = *(lds_i4)(uintptr_t)(ra + 16);
+        aab = *(lds_i1)(uintptr_t)ba;
+        symbol(b0, b1, bab, t + 1);
       }
+      if (t < cnt) symbol(a0, a1, aab, t);
+      state = (uint64_t)st_hi << 32 | st_lo;
       pos = ipos;
       flag |= ipos < 0 ? IDF_STREAM_UNDERFLOW : 0;  // ran out of words (pos never grows)
       outv = (float)(outi + lower_l) * 0.00390625f;
