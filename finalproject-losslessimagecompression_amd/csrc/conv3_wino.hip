@@ -70,6 +70,10 @@
 #ifndef IDF_X3_K32
 #define IDF_X3_K32 0
 #endif
+// timing-only in-kernel s_memtime stamps (tools/native/wino_ablate wino_stamps builds)
+#ifndef IDF_WINO_STAMPS
+#define IDF_WINO_STAMPS 0
+#endif
 namespace idf {
 
 typedef float w4 __attribute__((ext_vector_type(4)));
@@ -102,6 +106,7 @@ struct WinoArgs {
   float yscale;
   uint32_t* flag;  // X3: bit 0 set when the range guard trips
   int32_t check_in;  // X3: also range-check every transformed input V (block inputs)
+  int32_t vec4;      // epilogue may store 4 channels per 16-B store (out, ldo 16-B aligned)
 };
 
 // X3 range guard: |V| below this keeps hi = f16(V) finite (f16 max 65504) with margin.
@@ -125,6 +130,16 @@ __device__ __forceinline__ float wact(float v, int act, float slope) {
   if (act == IDF_ACT_LEAKY) return v > 0.0f ? v : v * slope;
   if (act == IDF_ACT_TANH) return tanhf(v);
   return v;
+}
+
+// a / b for 0 <= a < 2^20, 1 <= b < 2^20, exact: the float estimate is within 0.25 of a / b,
+// one remainder step corrects its truncation.  ~6 instructions instead of the ~35 of a
+// general 32-bit division: the kernel's index maps (halo slots, tiles, the block index) take
+// a dozen or more per thread, all before its first load.
+__device__ __forceinline__ int udiv_s(int a, int b) {
+  int q = (int)((float)a * __builtin_amdgcn_rcpf((float)b));
+  const int r = a - q * b;
+  return q + (r >= b) - (r < 0);
 }
 
 __device__ __forceinline__ float wbias(const WinoArgs& g, int n, int y, int x) {
@@ -427,24 +442,25 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   constexpr int BT_OFF = REGS && 2 * STAGE > MS ? 2 * STAGE : MS;
   __shared__ __attribute__((aligned(16))) float lds[LOOP_LDS > BT_OFF + BT ? LOOP_LDS : BT_OFF + BT];
 
+  const uint64_t st_k0 = IDF_WINO_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   int bid = blockIdx.x;
-  const int ks = bid % g.ksplit;
-  bid /= g.ksplit;
-  const int nt = bid % g.n_tiles;
-  bid /= g.n_tiles;
-  const int tx_ = bid % g.tiles_x;
-  bid /= g.tiles_x;
-  const int ty_ = bid % g.tiles_y;
-  const int tb = bid / g.tiles_y;
+  const int ks = bid - udiv_s(bid, g.ksplit) * g.ksplit;
+  bid = udiv_s(bid, g.ksplit);
+  const int nt = bid - udiv_s(bid, g.n_tiles) * g.n_tiles;
+  bid = udiv_s(bid, g.n_tiles);
+  const int tx_ = bid - udiv_s(bid, g.tiles_x) * g.tiles_x;
+  bid = udiv_s(bid, g.tiles_x);
+  const int tb = udiv_s(bid, g.tiles_y);
+  const int ty_ = bid - tb * g.tiles_y;
   const int b0 = tb * g.IMGS, y0 = ty_ * g.TH, x0 = tx_ * g.TW;
   const int HWp = g.TW + 2, HH = g.TH + 2, EH = HWp >> 1;  // TW even: HWp even
   const int NH = g.IMGS * HH * HWp;
   const int nxi = 4 * ((NH + 63) >> 6);  // halo DMA wave-instructions per slab
   const int TTH = g.TH >> 1, TTW = g.TW >> 1, TPI = TTH * TTW;  // wino tiles per image
-  const int s_lo = (int)((int64_t)ks * g.nslab / g.ksplit);
-  const int s_hi = (int)((int64_t)(ks + 1) * g.nslab / g.ksplit);
+  const int s_lo = udiv_s(ks * g.nslab, g.ksplit);
+  const int s_hi = udiv_s((ks + 1) * g.nslab, g.ksplit);
   const int nf0 = nt * NF;
 
   // ---- halo DMA: buffer resource over the block's images; out-of-range offsets read 0.
@@ -460,11 +476,11 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
     const int f = wave + 8 * m;
     x_src[m] = kWInvalid;
     if (f < nxi) {
-      const int q = f / nblk, slot = (f - q * nblk) * 64 + lane;
+      const int q = udiv_s(f, nblk), slot = (f - q * nblk) * 64 + lane;
       if (slot < NH) {
-        const int img = slot / (HH * HWp);
+        const int img = udiv_s(slot, HH * HWp);
         const int rem = slot - img * HH * HWp;
-        const int hy = rem / HWp, cs = rem - hy * HWp;
+        const int hy = udiv_s(rem, HWp), cs = rem - hy * HWp;
         const int hx = cs < EH ? 2 * cs : 2 * (cs - EH) + 1;
         const int y = y0 + hy - 1, x = x0 + hx - 1;
         if (b0 + img < g.B && y >= 0 && y < g.H && x >= 0 && x < g.Wd)
@@ -479,7 +495,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
     {
       const int f = wave + 8 * m;
       if (f < nxi) {
-        const int q = f / nblk, k = f - q * nblk;
+        const int q = udiv_s(f, nblk), k = f - q * nblk;
         const bool ok = x_src[m] != kWInvalid && c0 + 4 * q < g.C;
         const uint32_t off = ok ? x_src[m] + (uint32_t)c0 * 4u : kWInvalid;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_ptr_t)(St + (q * SLOTS + 64 * k) * 4),
@@ -497,7 +513,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
 #pragma unroll
   for (int m = 0; m < XI_PER_W; ++m) {
     const int f = wave + 8 * m;
-    const int q = f / nblk, k = f - q * nblk;
+    const int q = udiv_s(f, nblk), k = f - q * nblk;
     pc_dst[m] = f < nxi ? (q * SLOTS + 64 * k) * 4 : -1;
     pc_q4[m] = 4 * q;
   }
@@ -525,19 +541,13 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int t = 16 * i + lr;
-    int img = t / TPI;
+    int img = udiv_s(t, TPI);
     const int rem = t - img * TPI;
-    const int ty = rem / TTW, tx = rem - ty * TTW;
+    const int ty = udiv_s(rem, TTW), tx = rem - ty * TTW;
     if (img >= g.IMGS) img = 0;  // idle rows read valid LDS
     tbase[i] = (img * HH + 2 * ty) * HWp + tx;
   }
 
-  // REGS: the epilogue's bias table lies past the halo stages, so stage it now (its global
-  // loads' latency hides under the main loop; the loop's barriers publish it)
-  if constexpr (REGS) {
-    if (g.ksplit == 1)
-      stage_bias(lds + BT_OFF, NF * 16, nf0 * 16, g.N, g.b3, g.vtap, g.bfull, g.ldv, tid, kWThreads);
-  }
   w4 acc[4][2 * NF];  // [tile fragment][position q * NF + n-fragment]
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -669,9 +679,6 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
         u[q][j] = *(const w4*)(lds + 2 * STAGE + buf * USTAGE + ((2 * wave + q) * NF + j) * 256 +
                                lane * 4);
   };
-#ifndef IDF_WINO_STAMPS
-#define IDF_WINO_STAMPS 0
-#endif
   // timing-only instrumentation (tools/native/wino_ablate): cycles per wave in the barrier
   // waits, in the DMA issue after them, and in the whole loop -> g.part[block][wave][3]
   uint64_t st_wait = 0, st_issue = 0, st_t0 = 0;
@@ -802,9 +809,9 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
       hsrc[m] = kWInvalid;
       hdst[m] = (hq * SLOTS + (slot < SLOTS ? slot : SLOTS - 1)) * 4;  // slots >= NH: unused
       if (slot < NH) {
-        const int img = slot / (HH * HWp);
+        const int img = udiv_s(slot, HH * HWp);
         const int rem = slot - img * HH * HWp;
-        const int hy = rem / HWp, cs = rem - hy * HWp;
+        const int hy = udiv_s(rem, HWp), cs = rem - hy * HWp;
         const int hx = cs < EH ? 2 * cs : 2 * (cs - EH) + 1;
         const int y = y0 + hy - 1, x = x0 + hx - 1;
         if (b0 + img < g.B && y >= 0 && y < g.H && x >= 0 && x < g.Wd)
@@ -852,13 +859,22 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
     w4 d[2][6];
     h4 hl[2][4];
     w4 hb[XR_PER_W];
-    if (s_lo >= s_hi) return;
+    if (s_lo >= s_hi) {
+      if (g.ksplit == 1)
+        stage_bias(lds + BT_OFF, NF * 16, nf0 * 16, g.N, g.b3, g.vtap, g.bfull, g.ldv, tid, kWThreads);
+      return;
+    }
     if (IDF_WINO_STAMPS) st_t0 = __builtin_amdgcn_s_memtime();
+    if (IDF_WINO_STAMPS) st_issue = st_t0 - st_k0;  // prologue: kernel entry -> loop start
     // the second-dispatched half (waves 4-7) loses every issue arbitration to its older SIMD
     // partner at equal priority; one static raise evens the two (MI355X_MICROARCH.md)
     if (IDF_X3_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
     load_halo(s_lo, hb);
     load_ur(s_lo, ua);
+    // the epilogue's bias table lies past the halo stages: stage it while the first halo and
+    // U loads are in flight (one global round trip for both; the loop's barriers publish it)
+    if (g.ksplit == 1)
+      stage_bias(lds + BT_OFF, NF * 16, nf0 * 16, g.N, g.b3, g.vtap, g.bfull, g.ldv, tid, kWThreads);
     store_halo(0, hb);
     load_halo(s_lo + 1, hb);
     lds_barrier();
@@ -975,12 +991,14 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   float* obase = g.out ? g.out + pix0 * g.ldo : nullptr;
   float* pbase = g.part ? g.part + ((int64_t)ks * ((int64_t)g.B * g.H * g.Wd) + pix0) * g.ldp : nullptr;
   const float* rbase = g.res ? g.res + pix0 * g.ldr : nullptr;
+  const bool vec = REGS && g.ksplit == 1 && !g.res && g.vec4;
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
+    if (vec) break;  // the vector epilogue computes its own pixel map below
     const int t = (tid + kWThreads * it) >> 4;
-    const int img = t / TPI;
+    const int img = udiv_s(t, TPI);
     const int rem = t - img * TPI;
-    const int ty = rem / TTW, tx = rem - ty * TTW;
+    const int ty = udiv_s(rem, TTW), tx = rem - ty * TTW;
     e_img[it] = img;
 #pragma unroll
     for (int r = 0; r < 2; ++r)
@@ -991,6 +1009,26 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
         e_q[it][r][c] = ok ? (img * g.H + y) * g.Wd + x : -1;
         e_cls[it][r][c] = bias_class(y, x, g.H, g.Wd);
       }
+  }
+  // Vector epilogue (register-staged loop, no split-K, no residual, 16-B aligned output):
+  // thread = (tile v_t, channel quad v_nq, output row v_r); it finishes 4 channels of its
+  // tile's two pixels in that row and stores each pixel's 4 channels with one 16-B store --
+  // a quarter of the store instructions of one channel per thread, which made the epilogue
+  // store-issue-bound.  Same arithmetic, same order: bit-identical outputs.
+  const int v_t = tid >> 3, v_nq = (tid >> 1) & 3, v_r = tid & 1;
+  int v_q[2], v_cls[2], v_img;
+  {
+    const int img = udiv_s(v_t, TPI);
+    const int rem = v_t - img * TPI;
+    const int ty = udiv_s(rem, TTW), tx = rem - ty * TTW;
+    v_img = img;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int y = y0 + 2 * ty + v_r, x = x0 + 2 * tx + c;
+      const bool ok = img < g.IMGS && b0 + img < g.B && y < g.H && x < g.Wd;
+      v_q[c] = ok ? (img * g.H + y) * g.Wd + x : -1;
+      v_cls[c] = bias_class(y, x, g.H, g.Wd);
+    }
   }
   uint64_t st_e[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (IDF_WINO_STAMPS) st_e[0] = __builtin_amdgcn_s_memtime();
@@ -1029,6 +1067,48 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
     }
     epi_barrier();
     if (IDF_WINO_STAMPS) st_e[1 + 2 * j] = __builtin_amdgcn_s_memtime();
+    if (vec) {
+      const int nl = 4 * v_nq, n0 = (nf0 + j) * 16 + nl;
+      if (v_img < g.IMGS && n0 < g.N) {
+        float Y[2][4];  // [pixel c][channel k]
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          // row v_r of A^T m needs rows v_r .. v_r + 2 of m
+          const float* row = Ms + (nl + k) * ERW + v_t * 16 + 4 * v_r;
+          const w4 ma = *(const w4*)(row), mb = *(const w4*)(row + 4), mc = *(const w4*)(row + 8);
+          float u[4];
+#pragma unroll
+          for (int b = 0; b < 4; ++b)
+            u[b] = v_r == 0 ? (ma[b] + mb[b]) + mc[b] : (ma[b] - mb[b]) - mc[b];
+          Y[0][k] = (u[0] + u[1]) + u[2];
+          Y[1][k] = (u[1] - u[2]) - u[3];
+          if constexpr (X3) {
+            Y[0][k] = Y[0][k] * g.yscale;
+            Y[1][k] = Y[1][k] * g.yscale;
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int qp = v_q[c];
+          if (qp < 0) continue;
+          const w4 bv = *(const w4*)(btab + v_cls[c] * (NF * 16) + nl + j * 16);
+          w4 v;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            v[k] = wact(Y[c][k] + bv[k], g.act, g.slope);
+            if constexpr (X3) out_ok = out_ok && fabsf(v[k]) < kX3OutGuard;
+          }
+          float* dst = obase + (int64_t)qp * g.ldo + n0;
+          if (n0 + 4 <= g.N) {
+            *(w4*)dst = v;
+          } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              if (n0 + k < g.N) dst[k] = v[k];
+          }
+        }
+      }
+    } else
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       const int t = (tid + kWThreads * it) >> 4, nn = tid & 15;
@@ -1215,6 +1295,7 @@ static int wino_launch(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
   g.out = out; g.ldo = ld_out;
   g.res = res; g.ldr = ld_res;
   g.yscale = yscale; g.flag = x3 ? flag : nullptr; g.check_in = check_in;
+  g.vec4 = ((uintptr_t)out % 16 == 0) && (ld_out % 4 == 0);
   if (vtap && (!bfull || ldv < N)) return IDF_ERR_ARG;
   if (res && ld_res < N) return IDF_ERR_ARG;
   if (IDF_WINO_STAMPS) g.part = workspace;
@@ -1225,6 +1306,8 @@ static int wino_launch(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
     g.part = workspace;
   }
   const int64_t blocks = (int64_t)g.tiles_b * g.tiles_y * g.tiles_x * g.n_tiles * pl.ksplit;
+  // the kernel's index maps use udiv_s (operands < 2^20)
+  if (blocks >= (1 << 20) || (int64_t)(pl.ksplit + 1) * g.nslab >= (1 << 20)) return IDF_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
 #define IDF_WINO_LAUNCH(nf, slots, x3, chk)                                                     \
   hipLaunchKernelGGL((conv3_wino_kernel<nf, slots, x3, chk>), dim3((unsigned)blocks),              \

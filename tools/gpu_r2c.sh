@@ -12,6 +12,6 @@ tail -2 gpurun_out/r2c_smoke.log
 timeout -k 10 600 python -u bench.py > gpurun_out/r2c_bench.log 2>&1 || exit $?
 tail -c 2500 gpurun_out/r2c_bench.log
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r2c_prof -o run --output-format csv -- python -u bench.py --no-residual --no-cpu-baseline > gpurun_out/r2c_prof.log 2>&1 || exit $?
+timeout -k 10 60 ./tools/native/wino_stamps x3 > gpurun_out/r2c_conv_time.log 2>&1 && cat gpurun_out/r2c_conv_time.log && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r2c_prof -o run --output-format csv -- python -u bench.py --no-residual --no-cpu-baseline > gpurun_out/r2c_prof.log 2>&1 || exit $?
 find gpurun_out/r2c_prof -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} gpurun_out/r2c_kernel_stats.csv
 head -12 gpurun_out/r2c_kernel_stats.csv

@@ -16,6 +16,18 @@ static float* dev_random(size_t n) {
   return d;
 }
 
+// U for the split-f16 (x3) kernel: every float slot holds two small f16 values (random
+// float bits reinterpreted as f16 pairs would put NaN / inf in the products and make every
+// thread of the epilogue hit the range guard's atomic)
+static float* dev_random_f16pairs(size_t n) {
+  std::vector<_Float16> h(2 * n);
+  for (size_t i = 0; i < 2 * n; ++i) h[i] = (_Float16)(((float)rand() / RAND_MAX - 0.5f) * 0.05f);
+  float* d;
+  if (hipMalloc(&d, n * 4) != hipSuccess) abort();
+  if (hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess) abort();
+  return d;
+}
+
 int main(int argc, char** argv) {
   const bool x3 = argc > 1 && argv[1][0] == 'x';
   uint32_t* flag;
@@ -25,7 +37,8 @@ int main(int argc, char** argv) {
   for (auto& cs : cases) {
     const int P = cs.B * cs.hw * cs.hw, ld = (cs.c + N + 15) / 16 * 16, nslab = (cs.c + 15) / 16;
     float* X = dev_random((size_t)P * ld);
-    float* U = dev_random((size_t)16 * nslab * (n_alloc / 16) * 256);
+    float* U = x3 ? dev_random_f16pairs((size_t)16 * nslab * (n_alloc / 16) * 256)
+                  : dev_random((size_t)16 * nslab * (n_alloc / 16) * 256);
     float* b = dev_random(n_alloc * 10);
     const int64_t wsn = idf_conv3x3_wino_workspace(cs.B, cs.hw, cs.hw, cs.c, N);
     const int64_t nblk_dbg = (int64_t)cs.B * cs.hw * cs.hw / 64 * 8 * 12 + 4096;
@@ -59,7 +72,7 @@ int main(int argc, char** argv) {
           sw += h[(b * 8 + w) * 4]; si += h[(b * 8 + w) * 4 + 1]; st += h[(b * 8 + w) * 4 + 2];
           se += h[(b * 8 + w) * 4 + 3];
         }
-      printf("  stamps (memtime units/wave): loop %.0f  barrier-wait %.0f  dma-issue %.0f  epilogue %.0f\n",
+      printf("  stamps (memtime units/wave): loop %.0f  barrier-wait %.0f  prologue %.0f  epilogue %.0f\n",
              st / nb / 8, sw / nb / 8, si / nb / 8, se / nb / 8);
       double ep[8] = {0};
       for (int b = 0; b < nb; ++b)
