@@ -43,7 +43,7 @@
 // bit 0 skips the per-slab DMA, bit 1 skips the halo LDS reads, bit 2 skips the MFMAs,
 // bit 3 skips the input transform, bit 4 the in-loop barrier, bit 5 the U loads, bit 6
 // makes every halo DMA piece read 1 KiB of contiguous (wrong) memory, bit 8 (256) skips the
-// X3 f16 split.
+// X3 f16 split, 128 the epilogue's global stores, 1024 its staging reads.
 #ifndef IDF_WINO_ABLATE
 #define IDF_WINO_ABLATE 0
 #endif
@@ -439,7 +439,9 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   constexpr bool REGS = PIPE && IDF_X3_REGSTAGE;  // halo and U through registers (run_x3r)
   constexpr int LOOP_LDS = PIPE && !REGS ? DMA_SINK + 256 : 2 * STAGE;
   // REGS stages the epilogue bias table before the main loop: it must lie past the stages
-  constexpr int BT_OFF = REGS && 2 * STAGE > MS ? 2 * STAGE : MS;
+  // (REGS staging: 16 n rows of kERW floats, see the epilogue)
+  constexpr int MSR = REGS ? 16 * (64 * 20 + 4) : MS;
+  constexpr int BT_OFF = REGS && 2 * STAGE > MSR ? 2 * STAGE : MSR;
   __shared__ __attribute__((aligned(16))) float lds[LOOP_LDS > BT_OFF + BT ? LOOP_LDS : BT_OFF + BT];
 
   const uint64_t st_k0 = IDF_WINO_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
@@ -1015,7 +1017,10 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   // tile's two pixels in that row and stores each pixel's 4 channels with one 16-B store --
   // a quarter of the store instructions of one channel per thread, which made the epilogue
   // store-issue-bound.  Same arithmetic, same order: bit-identical outputs.
-  const int v_t = tid >> 3, v_nq = (tid >> 1) & 3, v_r = tid & 1;
+  // lane bits -> (tile, quad, row) chosen so that the staging reads are free of LDS bank
+  // conflicts with the 20-float tile pitch (every ds_read_b128 lane group hits 16 slots)
+  const int v_t = 8 * wave + (((lane >> 2) & 1) | (((lane >> 3) & 1) << 1) | ((lane & 1) << 2));
+  const int v_nq = ((lane >> 4) & 1) | (((lane >> 1) & 1) << 1), v_r = (lane >> 5) & 1;
   int v_q[2], v_cls[2], v_img;
   {
     const int img = udiv_s(v_t, TPI);
@@ -1033,10 +1038,10 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   uint64_t st_e[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (IDF_WINO_STAMPS) st_e[0] = __builtin_amdgcn_s_memtime();
   // ---- output transform, one n-fragment at a time through LDS
-  float* Ms = lds;  // [16 pos][64 tiles][kWMsPitch]; REGS: [16 n][64 tiles][16 pos] (+4 per n)
+  float* Ms = lds;  // [16 pos][64 tiles][kWMsPitch]; REGS: [16 n][64 tiles][20: 16 pos + pad] (+4 per n)
   float* btab = lds + BT_OFF;  // [16 border classes][NF * 16]
-  constexpr int ERW = 64 * 16 + 4;  // REGS staging: floats per n row (16-B pad: b64 writes,
-                                    // b128 reads at most 2-way conflicted)
+  constexpr int TPI_ = 20;           // REGS staging: floats per tile (16 positions + 4 pad)
+  constexpr int ERW = 64 * TPI_ + 4;  // REGS staging: floats per n row
   static_assert(!REGS || 16 * ERW <= BT_OFF, "REGS staging must fit below the bias table");
   if (g.ksplit == 1 && !REGS)
     stage_bias(btab, NF * 16, nf0 * 16, g.N, g.b3, g.vtap, g.bfull, g.ldv, tid, kWThreads);
@@ -1050,7 +1055,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
         for (int r = 0; r < 4; ++r) {
           const int t = 16 * i + (lane >> 4) * 4 + r;
           typedef float f2s __attribute__((ext_vector_type(2)));
-          *(f2s*)(Ms + lr * ERW + t * 16 + 2 * wave) = f2s{acc[i][j][r], acc[i][NF + j][r]};
+          *(f2s*)(Ms + lr * ERW + t * TPI_ + 2 * wave) = f2s{acc[i][j][r], acc[i][NF + j][r]};
         }
     } else {
 #pragma unroll
@@ -1074,8 +1079,13 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           // row v_r of A^T m needs rows v_r .. v_r + 2 of m
-          const float* row = Ms + (nl + k) * ERW + v_t * 16 + 4 * v_r;
-          const w4 ma = *(const w4*)(row), mb = *(const w4*)(row + 4), mc = *(const w4*)(row + 8);
+          const float* row = Ms + (nl + k) * ERW + v_t * TPI_ + 4 * v_r;
+          w4 ma, mb, mc;
+          if (IDF_WINO_ABLATE & 1024) {  // timing-only: no staging reads
+            ma = w4{(float)k, 1.f, 2.f, 3.f}; mb = ma; mc = ma;
+          } else {
+            ma = *(const w4*)(row); mb = *(const w4*)(row + 4); mc = *(const w4*)(row + 8);
+          }
           float u[4];
 #pragma unroll
           for (int b = 0; b < 4; ++b)
@@ -1099,7 +1109,9 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
             if constexpr (X3) out_ok = out_ok && fabsf(v[k]) < kX3OutGuard;
           }
           float* dst = obase + (int64_t)qp * g.ldo + n0;
-          if (n0 + 4 <= g.N) {
+          if (IDF_WINO_ABLATE & 128) {  // timing-only: no stores (a never-true guard)
+            if (v[0] == 12345.f) obase[0] = v[0];
+          } else if (n0 + 4 <= g.N) {
             *(w4*)dst = v;
           } else {
 #pragma unroll
@@ -1118,7 +1130,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
         if constexpr (REGS) {
 #pragma unroll
           for (int a = 0; a < 4; ++a) {
-            const w4 row = *(const w4*)(Ms + nn * ERW + t * 16 + 4 * a);
+            const w4 row = *(const w4*)(Ms + nn * ERW + t * TPI_ + 4 * a);
 #pragma unroll
             for (int b = 0; b < 4; ++b) m[a][b] = row[b];
           }
