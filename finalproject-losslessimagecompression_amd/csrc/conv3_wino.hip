@@ -59,7 +59,7 @@
 #define IDF_X3_REGSTAGE 1
 #endif
 #ifndef IDF_X3_PRIO
-#define IDF_X3_PRIO 1
+#define IDF_X3_PRIO 0
 #endif
 // X3 products: 1 = Vl.Uh (K=16) + (Vh.Uh + Vh.Ul) (one K=32 MFMA), 0 = three K=16 MFMAs.
 // Measured no faster (0.91 vs 0.90 ms over the kbench layers), so off.  Note: hipcc (ROCm
@@ -868,8 +868,9 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
     }
     if (IDF_WINO_STAMPS) st_t0 = __builtin_amdgcn_s_memtime();
     if (IDF_WINO_STAMPS) st_issue = st_t0 - st_k0;  // prologue: kernel entry -> loop start
-    // the second-dispatched half (waves 4-7) loses every issue arbitration to its older SIMD
-    // partner at equal priority; one static raise evens the two (MI355X_MICROARCH.md)
+    // optional static priority for the second-dispatched half (waves 4-7), which loses issue
+    // arbitration to its older SIMD partner at equal priority (MI355X_MICROARCH.md); off by
+    // default since the round-2 loop measured 1-3% faster without it (profiles/r02/ablate)
     if (IDF_X3_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
     load_halo(s_lo, hb);
     load_ur(s_lo, ua);
