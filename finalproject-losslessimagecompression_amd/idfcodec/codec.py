@@ -482,7 +482,12 @@ class ImageCodec:
                 go.record(main)
                 top = eng.nsplit - 1
                 stagger = os.environ.get("IDF_LANE_STAGGER", "event") != "none"
-                for i, st in enumerate(self._lane_streams(nl)):
+                # The host enqueues the lanes interleaved -- one step (a level's rANS decode, or
+                # one coupling) of each lane in turn -- so that every lane's launches reach the
+                # GPU early: enqueued lane after lane, the second lane's first kernel waited for
+                # the host to issue all ~500 launches of the first (profiles/r02/lanes/).
+                gens, streams = [], self._lane_streams(nl)
+                for i, st in enumerate(streams):
                     st.wait_event(go if (stagger or i == 0) else first)
                     if i == 0:
                         first = go
@@ -497,12 +502,23 @@ class ImageCodec:
                                                 img0=i * h, n_img=h, slot=i)
                         if l == top:
                             ev.record(st)
+                    ci = None if cond is None else cond[i * h:(i + 1) * h].contiguous()
+                    gens.append(eng.inverse_pm_steps(h, dec, cond=ci, slot=i))
+                    # lane i's first step (its top level's rANS decode) is enqueued before lane
+                    # i + 1 waits on the event it records
                     with torch.cuda.stream(st):
-                        ci = None if cond is None else cond[i * h:(i + 1) * h].contiguous()
-                        ws = eng.inverse_pm(h, dec, cond=ci, slot=i)
-                        finish(i, i * h, h, ws)
+                        next(gens[i])
                     go = staggered
-                for st in self._lane_streams(nl):
+                live = list(range(nl))
+                while live:
+                    for i in list(live):
+                        with torch.cuda.stream(streams[i]):
+                            try:
+                                next(gens[i])
+                            except StopIteration:
+                                finish(i, i * h, h, eng.workspace(h, i))
+                                live.remove(i)
+                for st in streams:
                     main.wait_stream(st)
         finally:
             if mode != prev:

@@ -476,6 +476,16 @@ class FlowEngine:
         """Top-down decoder (flows.py:118-152 order).  For each level l (top first):
         prior -> decode_level(l, ws) fills ws['lat'] level l -> flows backward ->
         unsqueeze.  The image lands in ws['img'] (pixel-major, ld 4)."""
+        steps = self.inverse_pm_steps(B, decode_level, cond, priors, slot)
+        for _ in steps:
+            pass
+        return self.workspace(B, slot)
+
+    def inverse_pm_steps(self, B: int, decode_level, cond=None, priors: bool = True,
+                         slot: int = 0):
+        """inverse_pm as a generator that yields after each level's decode_level and after
+        each coupling block, so that the host can interleave the enqueue of several decode
+        lanes (ImageCodec): all launches go to the stream current at the FIRST step."""
         L = lib()
         ws = self.workspace(B, slot)
         s = _lib.stream_ptr(self.device)
@@ -494,6 +504,7 @@ class FlowEngine:
                 else:
                     self._prior(ws, B, l, s, mean, logs, scale, ptr(x) + Lv.z * FLOAT, Lv.ldx)
             decode_level(l, ws)
+            yield l
             check(L.idf_nchw_to_pm(s, B, Lv.z, Lv.h, Lv.w, ptr(ws["lat"]) + o * FLOAT, ptr(x),
                                    Lv.ldx), "nchw_to_pm")
             x2 = self._x(ws, l, 1)
@@ -511,6 +522,7 @@ class FlowEngine:
                 check(L.idf_permute_couple_in(s, P, Lv.C, ptr(self.inv_ids[l][k]), ptr(x), Lv.ldx,
                                               ptr(x2), Lv.ldx, 0, 0, None, 0), "permute")
                 self._swap(ws, l)
+                yield l
             x = self._x(ws, l)
             if l > 0:
                 Lp = self.levels[l - 1]
@@ -520,7 +532,6 @@ class FlowEngine:
                 dst, ldd, Hh, Ww, Cc = ptr(ws["img"]), 4, self.H, self.W, self.C
             check(L.idf_unsqueeze(s, B, Hh, Ww, Cc, self.scale, ptr(x), Lv.ldx, dst, ldd),
                   "unsqueeze")
-        return ws
 
     def image_nchw(self, ws, B, out=None):
         if out is None:
