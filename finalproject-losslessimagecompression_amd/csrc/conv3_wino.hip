@@ -70,6 +70,9 @@
 #ifndef IDF_X3_K32
 #define IDF_X3_K32 0
 #endif
+#ifndef IDF_X3_FAKE32
+#define IDF_X3_FAKE32 0
+#endif
 // timing-only in-kernel s_memtime stamps (tools/native/wino_ablate wino_stamps builds)
 #ifndef IDF_WINO_STAMPS
 #define IDF_WINO_STAMPS 0
@@ -372,8 +375,28 @@ struct WinoRole {
       gmax = valid ? fmaxf(gmax, m) : gmax;
     }
   }
+  template <int STEP = 0>
   __device__ __forceinline__ static void mfma_hl(const h4 (&hl)[4], const w4 (&u)[2][NF],
                                                  w4 (&acc)[NF * 2]) {
+#if IDF_X3_FAKE32
+    // timing-only (tools/native): the K=32 MFMA count of a slab-paired split-f16 scheme,
+    // 1.5 v_mfma_f32_16x16x32_f16 per (position, n-fragment) and step; results are wrong
+    {
+      const h8 a0 = __builtin_shufflevector(hl[0], hl[1], 0, 1, 2, 3, 4, 5, 6, 7);
+      const h8 a1 = __builtin_shufflevector(hl[2], hl[3], 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+      for (int jn = 0; jn < NF; ++jn) {
+        const h8 ua = __builtin_bit_cast(h8, u[0][jn]), ub = __builtin_bit_cast(h8, u[1][jn]);
+        acc[jn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, ua, acc[jn], 0, 0, 0);
+        acc[NF + jn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, ub, acc[NF + jn], 0, 0, 0);
+        if constexpr (STEP % 2 == 0) {
+          acc[jn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, ua, acc[jn], 0, 0, 0);
+          acc[NF + jn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, ub, acc[NF + jn], 0, 0, 0);
+        }
+      }
+      return;
+    }
+#endif
     if constexpr (IDF_X3_K32) {
       // Vl.Uh on v_mfma_f32_16x16x16_f16, then Vh.Uh + Vh.Ul as ONE
       // v_mfma_f32_16x16x32_f16: k = 8*quad + j takes A = (Vh, Vh) against the lane's
@@ -911,13 +934,13 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
         // the halo offsets are immediates (TWC > 0): one address add per fetch
         if constexpr (i < 2) role.fetch_p(pb[i + 2] + qoff, d[i & 1]);
         else role.fetch_p(pb[i - 2] + noff, d[i & 1]);
-        role.mfma_hl(hl[i & 1], ucur, acc[i]);
+        role.template mfma_hl<i>(hl[i & 1], ucur, acc[i]);
         {
           constexpr int ND = 6;
           constexpr int nvm = i == 0 ? 2 * NF : (i == 2 ? XR_PER_W : 0);
           constexpr int nst = i == 1 ? XR_PER_W : 0;
 #pragma unroll
-          for (int k = 0; k < (IDF_X3_K32 ? 4 : 6) * NF; ++k) {
+          for (int k = 0; k < (IDF_X3_FAKE32 ? (i % 2 == 0 ? 4 : 2) : (IDF_X3_K32 ? 4 : 6)) * NF; ++k) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
             if (k < ND) {
               __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
