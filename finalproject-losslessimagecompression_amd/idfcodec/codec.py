@@ -399,6 +399,15 @@ class ImageCodec:
             n -= 1
         return n
 
+    def _lane_sizes(self, B: int, n: int):
+        """Images per lane: equal (measured best), or with 2 lanes lane 0 takes IDF_LANE_SPLIT
+        of the batch (a smaller lane 0 runs ahead of lane 1; 112/144 decoded 1 ms slower)."""
+        f = float(os.environ.get("IDF_LANE_SPLIT", "0.5"))
+        if n == 2 and f != 0.5:
+            n0 = max(self.LANE_MIN, min(B - self.LANE_MIN, int(round(B * f))))
+            return [n0, B - n0]
+        return [B // n] * n
+
     def _lane_streams(self, n: int):
         while len(self._streams) < n:
             self._streams.append(_lib.new_stream(self.engine.device))
@@ -462,7 +471,8 @@ class ImageCodec:
                 self._lane_streams(nl)
             except (OSError, AttributeError, _lib.IdfError):
                 nl = 1  # no separate HIP streams: decode in one lane (same bits)
-        h = B // nl
+        sz = self._lane_sizes(B, nl)
+        off = [sum(sz[:i]) for i in range(nl)]
         # the convs must run as the encoder ran them (bit-identical couplings)
         mode, prev = bs.meta.get("conv", "f32"), eng.conv_mode
         if mode not in ("x3", "f32"):  # a fixed family, checked equal in check_bitstream
@@ -477,18 +487,27 @@ class ImageCodec:
                 finish(0, 0, B, ws)
             else:
                 main = torch.cuda.current_stream(eng.device)
-                eng.ensure_top_prior(eng.workspace(h, 0), _lib.stream_ptr(eng.device))
+                eng.ensure_top_prior(eng.workspace(sz[0], 0), _lib.stream_ptr(eng.device))
                 go = torch.cuda.Event()
                 go.record(main)
                 top = eng.nsplit - 1
-                stagger = os.environ.get("IDF_LANE_STAGGER", "event") != "none"
+                # IDF_LANE_STAGGER: "top" (default) -- lane i+1 starts after lane i's top-level
+                # rANS decode; "levels" -- also every other level's decode waits for lane i's
+                # decode of that level; "none" -- no cross-lane order.  The lanes drift
+                # together after the top level (the GPU ran only rANS kernels for 3.7 ms of a
+                # 31 ms decode), but neither "levels", a high-priority lane 0 nor unequal lanes
+                # (IDF_LANE_SPLIT) shortened the decode (profiles/r02/lanes/order_ab.txt).
+                stagger = os.environ.get("IDF_LANE_STAGGER", "top")
                 # The host enqueues the lanes interleaved -- one step (a level's rANS decode, or
                 # one coupling) of each lane in turn -- so that every lane's launches reach the
                 # GPU early: enqueued lane after lane, the second lane's first kernel waited for
-                # the host to issue all ~500 launches of the first (profiles/r02/lanes/).
+                # the host to issue all ~500 launches of the first (profiles/r02/lanes/).  Every
+                # lane has the same steps, so lane i-1's decode of a level is enqueued (its
+                # event recorded) before lane i's waits on it.
                 gens, streams = [], self._lane_streams(nl)
+                done = [dict() for _ in range(nl)]  # done[i][l]: lane i decoded level l
                 for i, st in enumerate(streams):
-                    st.wait_event(go if (stagger or i == 0) else first)
+                    st.wait_event(go if (stagger != "none" or i == 0) else first)
                     if i == 0:
                         first = go
                     if self.lane_marks is not None:  # lane start times (tools/lanes_probe.py)
@@ -498,12 +517,17 @@ class ImageCodec:
                     staggered = torch.cuda.Event()
 
                     def dec(l, ws, i=i, st=st, ev=staggered):
+                        if stagger == "levels" and i > 0 and l != top:
+                            st.wait_event(done[i - 1][l])
                         self.coder.decode_level(bs, B, l, ws, word_off, out_state, out_status,
-                                                img0=i * h, n_img=h, slot=i)
+                                                img0=off[i], n_img=sz[i], slot=i)
                         if l == top:
                             ev.record(st)
-                    ci = None if cond is None else cond[i * h:(i + 1) * h].contiguous()
-                    gens.append(eng.inverse_pm_steps(h, dec, cond=ci, slot=i))
+                        elif stagger == "levels":
+                            done[i][l] = torch.cuda.Event()
+                            done[i][l].record(st)
+                    ci = None if cond is None else cond[off[i]:off[i] + sz[i]].contiguous()
+                    gens.append(eng.inverse_pm_steps(sz[i], dec, cond=ci, slot=i))
                     # lane i's first step (its top level's rANS decode) is enqueued before lane
                     # i + 1 waits on the event it records
                     with torch.cuda.stream(st):
@@ -516,7 +540,7 @@ class ImageCodec:
                             try:
                                 next(gens[i])
                             except StopIteration:
-                                finish(i, i * h, h, eng.workspace(h, i))
+                                finish(i, off[i], sz[i], eng.workspace(sz[i], i))
                                 live.remove(i)
                 for st in streams:
                     main.wait_stream(st)

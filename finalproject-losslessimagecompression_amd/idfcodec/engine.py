@@ -310,7 +310,7 @@ class FlowEngine:
     # ------------------------------------------------------------ workspace
     def workspace(self, B: int, slot: int = 0):
         """Activation / latent buffers for B images.  Each slot is an independent set (the
-        ImageCodec lanes run one slot per HIP stream); one batch size stays resident."""
+        ImageCodec lanes run one slot per HIP stream); the four most recent sets stay resident."""
         ws = self._ws.get((B, slot))
         if ws is not None:
             return ws
@@ -332,7 +332,9 @@ class FlowEngine:
             ws["cond"] = [f(B * L.h * L.w * round_up(L.cond_ch, 4)) for L in self.levels]
             # channels C..3 of the 4-wide pixel rows stay zero (they meet zero weights)
             ws["cond_img"] = torch.zeros(B * self.H * self.W * 4, dtype=torch.float32, device=dev)
-        self._ws = {k: v for k, v in self._ws.items() if k[0] == B}  # one batch size resident
+        # the last few sets stay resident (an encode batch plus the decode lanes' sub-batches)
+        while len(self._ws) >= 4:
+            self._ws.pop(next(iter(self._ws)))
         self._ws[(B, slot)] = ws
         return ws
 

@@ -31,6 +31,22 @@ def test_lanes_decode_identical(B):
         assert torch.equal(out, img), lanes
         assert torch.equal(info["final_states"], rinfo["final_states"])
         assert torch.equal(info["status"], rinfo["status"])
+    # unequal lanes (IDF_LANE_SPLIT) under each cross-lane order (IDF_LANE_STAGGER)
+    import os
+    saved = {k: os.environ.get(k) for k in ("IDF_LANE_SPLIT", "IDF_LANE_STAGGER")}
+    try:
+        for split, stagger in (("0.375", "levels"), ("0.375", "top"), ("0.625", "none")):
+            os.environ["IDF_LANE_SPLIT"], os.environ["IDF_LANE_STAGGER"] = split, stagger
+            out, info = _decode_all(codec, bs, 2)
+            assert info["ok"] and torch.equal(out, img), (split, stagger)
+            assert torch.equal(info["final_states"], rinfo["final_states"])
+            assert torch.equal(info["status"], rinfo["status"])
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     # through the container, with the non-compact (scratch-offset) bitstream as well
     bs2 = Bitstream.from_bytes(bs.to_bytes(), device="cuda")
     out, info = _decode_all(codec, bs2, 2)

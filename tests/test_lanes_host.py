@@ -18,6 +18,17 @@ def test_lane_split():
     assert c._n_lanes(256) == 1
 
 
+def test_lane_sizes(monkeypatch):
+    c = ImageCodec(engine=None, lanes=2)
+    monkeypatch.delenv("IDF_LANE_SPLIT", raising=False)
+    assert c._lane_sizes(256, 2) == [128, 128]
+    assert c._lane_sizes(24, 3) == [8, 8, 8]
+    monkeypatch.setenv("IDF_LANE_SPLIT", "0.4375")
+    assert c._lane_sizes(256, 2) == [112, 144]
+    assert c._lane_sizes(16, 2) == [8, 8]      # clamped to LANE_MIN images per lane
+    assert c._lane_sizes(24, 3) == [8, 8, 8]   # the split applies to 2 lanes only
+
+
 def test_bench_rans_roofline_accounting():
     """bench.py's rANS line: algorithmic bytes (12 B/symbol + 4 B/word + 16 B/stream) over the
     summed launch time, ns per symbol of a stream's chain."""
