@@ -135,6 +135,22 @@ __device__ __forceinline__ float wact(float v, int act, float slope) {
   return v;
 }
 
+// wact without a branch per value (the epilogue's ReLU / LeakyReLU / identity): the same bits
+// as wact for those three -- v > 0 keeps v; else ReLU gives +0, LeakyReLU v * slope, identity
+// v * 1 = v (NaN: +0 for ReLU, NaN otherwise, as wact).  Tanh layers take wact.
+struct WAct {
+  float mul;   // v <= 0: v * mul (LeakyReLU slope, identity 1)
+  bool zero;   // ReLU
+  bool tanh_;
+  __device__ explicit WAct(int act, float slope)
+      : mul(act == IDF_ACT_LEAKY ? slope : 1.0f), zero(act == IDF_ACT_RELU),
+        tanh_(act == IDF_ACT_TANH) {}
+  __device__ __forceinline__ float operator()(float v) const {
+    const float neg = zero ? 0.0f : v * mul;
+    return v > 0.0f ? v : neg;
+  }
+};
+
 // a / b for 0 <= a < 2^20, 1 <= b < 2^20, exact: the float estimate is within 0.25 of a / b,
 // one remainder step corrects its truncation.  ~6 instructions instead of the ~35 of a
 // general 32-bit division: the kernel's index maps (halo slots, tiles, the block index) take
@@ -1004,6 +1020,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   }
 
   bool out_ok = true;  // X3: every stored output within kX3OutGuard (false on NaN)
+  const WAct act(g.act, g.slope);
   const uint64_t st_epi = IDF_WINO_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
 
   // LDS-only barrier for the epilogue: __syncthreads() would also drain every global store
@@ -1127,10 +1144,16 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
           if (qp < 0) continue;
           const w4 bv = *(const w4*)(btab + v_cls[c] * (NF * 16) + nl + j * 16);
           w4 v;
+          if (act.tanh_) {
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            v[k] = wact(Y[c][k] + bv[k], g.act, g.slope);
-            if constexpr (X3) out_ok = out_ok && fabsf(v[k]) < kX3OutGuard;
+            for (int k = 0; k < 4; ++k) v[k] = wact(Y[c][k] + bv[k], g.act, g.slope);
+          } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = act(Y[c][k] + bv[k]);
+          }
+          if constexpr (X3) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) out_ok = out_ok && fabsf(v[k]) < kX3OutGuard;
           }
           float* dst = obase + (int64_t)qp * g.ldo + n0;
           if (IDF_WINO_ABLATE & 128) {  // timing-only: no stores (a never-true guard)
@@ -1200,7 +1223,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
             if (g.ksplit == 1) {
               float v = Y[r][c] + btab[e_cls[it][r][c] * (NF * 16) + n - nf0 * 16];
               if (g.res) v = rv[r][c] + v;
-              v = wact(v, g.act, g.slope);
+              v = act.tanh_ ? wact(v, g.act, g.slope) : act(v);
               if constexpr (X3) out_ok = out_ok && fabsf(v) < kX3OutGuard;
               if (!(IDF_WINO_ABLATE & 128)) obase[(int64_t)qp * g.ldo + n] = v;
               else if (v == 12345.f) obase[0] = v;

@@ -1,7 +1,12 @@
 // Timing-only ablation harness for the Winograd conv kernel: built once per
 // IDF_WINO_ABLATE value (tools/native/Makefile), times the imagenet64 level-0 and level-2
 // widest layers on random data.  Outputs are meaningless for ablate != 0.
+// WINO_SRC: an alternative copy of the kernel source (same-box A/B against a baseline)
+#ifdef WINO_SRC
+#include WINO_SRC
+#else
 #include "../../finalproject-losslessimagecompression_amd/csrc/conv3_wino.hip"
+#endif
 
 #include <stdio.h>
 #include <stdlib.h>
