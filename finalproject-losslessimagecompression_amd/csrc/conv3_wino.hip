@@ -1086,47 +1086,47 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   static_assert(!REGS || 16 * ERW <= BT_OFF, "REGS staging must fit below the bias table");
   if (g.ksplit == 1 && !REGS)
     stage_bias(btab, NF * 16, nf0 * 16, g.N, g.b3, g.vtap, g.bfull, g.ldv, tid, kWThreads);
+  // REGS staging write of n-fragment j: a wave's two positions are adjacent, one 8-B write
+  // per (tile fragment, row)
+  auto write_regs = [&](auto jc) {
+    constexpr int j = decltype(jc)::value;
 #pragma unroll
-  for (int j = 0; j < NF; ++j) {
-    if constexpr (REGS) {
-      // a wave's two positions are adjacent: one 8-B write per (tile fragment, row)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int t = 16 * i + (lane >> 4) * 4 + r;
-          typedef float f2s __attribute__((ext_vector_type(2)));
-          *(f2s*)(Ms + lr * ERW + t * TPI_ + 2 * wave) = f2s{acc[i][j][r], acc[i][NF + j][r]};
-        }
-    } else {
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int p = 2 * wave + q;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int t = 16 * i + (lane >> 4) * 4 + r;
-            Ms[(p * 64 + t) * kWMsPitch + lr] = acc[i][q * NF + j][r];
-          }
+      for (int r = 0; r < 4; ++r) {
+        const int t = 16 * i + (lane >> 4) * 4 + r;
+        typedef float f2s __attribute__((ext_vector_type(2)));
+        *(f2s*)(Ms + lr * ERW + t * TPI_ + 2 * wave) = f2s{acc[i][j][r], acc[i][NF + j][r]};
       }
-    }
-    epi_barrier();
-    if (IDF_WINO_STAMPS) st_e[1 + 2 * j] = __builtin_amdgcn_s_memtime();
+  };
+  if constexpr (REGS) {
     if (vec) {
-      const int nl = 4 * v_nq, n0 = (nf0 + j) * 16 + nl;
-      if (v_img < g.IMGS && n0 < g.N) {
-        float Y[2][4];  // [pixel c][channel k]
+      // Vector epilogue, software-pipelined over the n-fragments: fragment j's staging reads
+      // land in registers (R) before the barrier that frees the staging for j + 1, and
+      // fragment j's arithmetic and stores run after this wave has issued its writes of
+      // j + 1 -- beside the other waves' writes instead of between two barriers.
+      w4 R[4][3];
+      auto read_frag = [&](int j) {
+        const int nl = 4 * v_nq;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           // row v_r of A^T m needs rows v_r .. v_r + 2 of m
           const float* row = Ms + (nl + k) * ERW + v_t * TPI_ + 4 * v_r;
-          w4 ma, mb, mc;
           if (IDF_WINO_ABLATE & 1024) {  // timing-only: no staging reads
-            ma = w4{(float)k, 1.f, 2.f, 3.f}; mb = ma; mc = ma;
+            R[k][0] = w4{(float)k, 1.f, 2.f, 3.f}; R[k][1] = R[k][0]; R[k][2] = R[k][0];
           } else {
-            ma = *(const w4*)(row); mb = *(const w4*)(row + 4); mc = *(const w4*)(row + 8);
+            R[k][0] = *(const w4*)(row); R[k][1] = *(const w4*)(row + 4);
+            R[k][2] = *(const w4*)(row + 8);
           }
+        }
+      };
+      auto finish_frag = [&](int j) {
+        const int nl = 4 * v_nq, n0 = (nf0 + j) * 16 + nl;
+        if (!(v_img < g.IMGS && n0 < g.N)) return;
+        float Y[2][4];  // [pixel c][channel k]
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const w4 ma = R[k][0], mb = R[k][1], mc = R[k][2];
           float u[4];
 #pragma unroll
           for (int b = 0; b < 4; ++b)
@@ -1166,8 +1166,52 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
               if (n0 + k < g.N) dst[k] = v[k];
           }
         }
+      };
+      auto frag = [&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        write_regs(jc);
+        if constexpr (j > 0) finish_frag(j - 1);
+        epi_barrier();
+        if (IDF_WINO_STAMPS) st_e[1 + 2 * j] = __builtin_amdgcn_s_memtime();
+        read_frag(j);
+        epi_barrier();  // the reads landed; every wave is done with the staging
+        if (IDF_WINO_STAMPS) st_e[2 + 2 * j] = __builtin_amdgcn_s_memtime();
+      };
+      frag(std::integral_constant<int, 0>{});
+      if constexpr (NF > 1) frag(std::integral_constant<int, 1>{});
+      if constexpr (NF > 2) frag(std::integral_constant<int, 2>{});
+      static_assert(NF <= 3, "vector epilogue: at most 3 n-fragments");
+      finish_frag(NF - 1);
+    }
+  }
+  if (!vec) {
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    if constexpr (REGS) {
+      // a wave's two positions are adjacent: one 8-B write per (tile fragment, row)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int t = 16 * i + (lane >> 4) * 4 + r;
+          typedef float f2s __attribute__((ext_vector_type(2)));
+          *(f2s*)(Ms + lr * ERW + t * TPI_ + 2 * wave) = f2s{acc[i][j][r], acc[i][NF + j][r]};
+        }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int p = 2 * wave + q;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int t = 16 * i + (lane >> 4) * 4 + r;
+            Ms[(p * 64 + t) * kWMsPitch + lr] = acc[i][q * NF + j][r];
+          }
       }
-    } else
+    }
+    epi_barrier();
+    if (IDF_WINO_STAMPS) st_e[1 + 2 * j] = __builtin_amdgcn_s_memtime();
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       const int t = (tid + kWThreads * it) >> 4, nn = tid & 15;
@@ -1235,6 +1279,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
     }
     if (IDF_WINO_STAMPS) st_e[2 + 2 * j] = __builtin_amdgcn_s_memtime();
     epi_barrier();
+  }
   }
   if constexpr (X3) {
     if (!out_ok && g.flag) atomicOr(g.flag, 1u);
