@@ -75,31 +75,37 @@ def launch(args) -> int:
     return subprocess.call(cmd)
 
 
-def pmc_traffic(kernel: str):
+def pmc_traffic(kernel: str, n_last: int, extra: str = "conv3_wino_reduce_kernel"):
     """HBM bytes per launch of `kernel` from the newest committed PMC passes
     (profiles/<round>/pmc_bench/{fetch,write}.csv, written by tools/pmc_bench.sh over this
-    bench): mean over its dispatches of 2 x FETCH_SIZE (the gfx950 correction for
-    16-B-per-lane streaming reads, MI355X_MICROARCH.md "HBM") + WRITE_SIZE, KiB -> bytes.
-    None when no such profile exists."""
+    bench), over the same launches as roofline.achieved: the process's last n_last dispatches
+    whose name contains `kernel` (the sampled encode pass ends the run) plus the `extra`
+    dispatches among them (the 8x8 split-K reduce, whose time roofline_pass also counts).
+    Bytes = 2 x FETCH_SIZE (the gfx950 correction for 16-B-per-lane streaming reads,
+    MI355X_MICROARCH.md "HBM") + WRITE_SIZE, KiB -> bytes.  None when no such profile exists."""
     import csv
     import glob
     fetch = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_bench", "fetch.csv")))
-    if not fetch:
+    if not fetch or n_last <= 0:
         return None, None
     d = os.path.dirname(fetch[-1])
 
-    def mean(name):
+    def total(name):
         path = os.path.join(d, name)
         if not os.path.exists(path):
             return None
-        v = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-             if kernel in r["Kernel_Name"]]
-        return sum(v) / len(v) if v else None
-    f, w = mean("fetch.csv"), mean("write.csv")
+        rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Dispatch_Id"]))
+        main = [r for r in rows if kernel in r["Kernel_Name"]]
+        if len(main) < n_last:
+            return None
+        d0 = int(main[-n_last]["Dispatch_Id"])
+        sel = main[-n_last:] + [r for r in rows if extra and extra in r["Kernel_Name"]
+                                and int(r["Dispatch_Id"]) >= d0]
+        return sum(float(r["Counter_Value"]) for r in sel)
+    f, w = total("fetch.csv"), total("write.csv")
     if f is None or w is None:
         return None, None
-    return (2.0 * f + w) * 1024.0, os.path.relpath(d, REPO)
-
+    return (2.0 * f + w) * 1024.0 / n_last, os.path.relpath(d, REPO)
 
 def rans_roofline(trace, bs, steps):
     """rANS encode / decode (prep + serial pass per launch pair), timed with HIP events on
@@ -252,6 +258,22 @@ def cpu_baseline(model_cfg, n_img, runs, chunk=16):
                        f"round trips exact={exact}")}
 
 
+def conv_algorithmic_bytes(eng, B):
+    """(launches, algorithmic HBM bytes) of one encode's DenseLayer convs -- the launches
+    roofline_pass times: per launch the layer's c input channels read and g outputs written,
+    fp32, per pixel, plus its Winograd weights (16 positions x c x g f16 hi/lo pairs, 4 B)."""
+    n = byt = 0
+    for l, L in enumerate(eng.levels):
+        P = B * L.h * L.w
+        for geom in [b.geom for b in eng.couple[l]] + [eng.prior[l].geom]:
+            c = geom.a
+            for g in geom.growth:
+                n += 1
+                byt += 4 * P * (c + g) + 16 * c * g * 4
+                c += g
+    return n, byt
+
+
 def roofline_pass(codec, eng, timer, img):
     """The dominant kernel timed live: one encode of the batch after the timed steps, with the
     side-stream rANS encode off (every conv launch has the chip to itself) and HIP events
@@ -394,9 +416,12 @@ def main():
     _lib.lib().idf_timer_destroy(timer)
 
     flops = eng.flops_per_image()["total"]
-    kname = ("conv3_wino_kernel<3, 448, true, false," if eng.conv_mode == "x3"
+    # both range-check variants of the kernel: roofline_pass times every DenseLayer conv launch
+    kname = ("conv3_wino_kernel<3, 448, true," if eng.conv_mode == "x3"
              else "conv3_wino_kernel<3, 448, false")
-    traffic, traffic_src = pmc_traffic(kname) if eng.wino else (None, None)
+    traffic, traffic_src = pmc_traffic(kname, c3_n) if eng.wino else (None, None)
+    n_algo, b_algo = conv_algorithmic_bytes(eng, B)
+    algo_bytes = b_algo / n_algo if n_algo == c3_n and n_algo else None
     # the x3 kernel's products run on f16 MFMA: price them against the f16 dense peak
     peak = PEAK_F16_TFLOPS if (eng.wino and eng.conv_mode == "x3") else PEAK_F32_TFLOPS
     flops_exec = eng.flops_per_image(fold=eng.fold)["total"]
@@ -468,6 +493,9 @@ def main():
                 "traffic": traffic,
                 "traffic_unit": "B/launch (HBM, PMC)",
                 "traffic_source": traffic_src,
+                "algorithmic_bytes_per_launch": algo_bytes,
+                "traffic_over_algorithmic": (round(traffic / algo_bytes, 3)
+                                             if traffic and algo_bytes else None),
                 "avg_launch_ms": round(c3_avg_ms, 5),
                 "mfma_executed_tflops": round(c3_tflops * exec_ratio, 3),
                 "mfma_executed_frac": round(c3_tflops * exec_ratio / peak, 4),

@@ -229,6 +229,13 @@ __device__ __forceinline__ void split_f16(const w4& v, h4& h, h4& l) {
   l = __builtin_bit_cast(h4, u2{la, lb});
 }
 
+// Halo row pitch (slots) for an output tile TW wide: TW + 2, plus 2 when a 16-tile MFMA
+// fragment spans two rows of 8 tiles (TW = 16).  Its two rows' slots then differ by 8 mod 16
+// and every ds_read_b128 lane group of the halo reads hits 16 distinct bank quads; at 18 they
+// differed by 36 = 4 mod 16 and half of the group collided (SQ_LDS_BANK_CONFLICT 2x the LDS
+// cycles of the 16x16 level).  TW = 32 fragments lie in one tile row; TW = 8 rows land 0/4/8/12.
+__host__ __device__ constexpr int halo_pitch(int tw) { return tw + 2 + (tw == 16 ? 2 : 0); }
+
 // Column slot of halo column j (0..3) relative to a tile's even-half base, de-interleaved.
 __device__ __forceinline__ int colslot(int j, int EH) { return (j & 1) ? EH + (j >> 1) : (j >> 1); }
 
@@ -244,7 +251,7 @@ struct WinoRole {
   using C1 = BT<2 * BP + 1>;
   // the three halo columns the pair needs: {0,1,2} (BP=0) or {1,2,3} (BP=1)
   static constexpr int j0 = BP, j1 = BP + 1, j2 = BP + 2;
-  static constexpr int HWc = TWC + 2, EHc = HWc / 2;
+  static constexpr int HWc = halo_pitch(TWC), EHc = HWc / 2;
   static constexpr int csc(int j) { return (j & 1) ? EHc + (j >> 1) : (j >> 1); }
   static constexpr int oc(int e) {
     return ((e < 3 ? RA::i0 : RA::i1) * HWc + csc(e % 3 == 0 ? j0 : (e % 3 == 1 ? j1 : j2))) * 4;
@@ -496,7 +503,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   const int tb = udiv_s(bid, g.tiles_y);
   const int ty_ = bid - tb * g.tiles_y;
   const int b0 = tb * g.IMGS, y0 = ty_ * g.TH, x0 = tx_ * g.TW;
-  const int HWp = g.TW + 2, HH = g.TH + 2, EH = HWp >> 1;  // TW even: HWp even
+  const int HWp = halo_pitch(g.TW), HH = g.TH + 2, EH = HWp >> 1;  // TW even: HWp even
   const int NH = g.IMGS * HH * HWp;
   const int nxi = 4 * ((NH + 63) >> 6);  // halo DMA wave-instructions per slab
   const int TTH = g.TH >> 1, TTW = g.TW >> 1, TPI = TTH * TTW;  // wino tiles per image
@@ -524,7 +531,8 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
         const int hy = udiv_s(rem, HWp), cs = rem - hy * HWp;
         const int hx = cs < EH ? 2 * cs : 2 * (cs - EH) + 1;
         const int y = y0 + hy - 1, x = x0 + hx - 1;
-        if (b0 + img < g.B && y >= 0 && y < g.H && x >= 0 && x < g.Wd)
+        // hx >= TW + 2: a pitch pad slot (never read)
+        if (b0 + img < g.B && y >= 0 && y < g.H && x >= 0 && x < g.Wd && hx < g.TW + 2)
           x_src[m] = (uint32_t)(((((int64_t)img * g.H + y) * g.Wd + x) * g.ldx + 4 * q) * 4);
         if (IDF_WINO_ABLATE & 64) x_src[m] = (uint32_t)((f * 64 + lane) * 16);  // coalesced, wrong
       }
@@ -855,7 +863,8 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
         const int hy = udiv_s(rem, HWp), cs = rem - hy * HWp;
         const int hx = cs < EH ? 2 * cs : 2 * (cs - EH) + 1;
         const int y = y0 + hy - 1, x = x0 + hx - 1;
-        if (b0 + img < g.B && y >= 0 && y < g.H && x >= 0 && x < g.Wd)
+        // hx >= TW + 2: a pitch pad slot (never read)
+        if (b0 + img < g.B && y >= 0 && y < g.H && x >= 0 && x < g.Wd && hx < g.TW + 2)
           hsrc[m] = (uint32_t)(((((int64_t)img * g.H + y) * g.Wd + x) * g.ldx + 4 * hq) * 4);
       }
     }
@@ -1335,7 +1344,7 @@ static WinoPlan wino_plan(int H, int W, int nslab, int N) {
     pl.IMGS = 256 / (pl.TH * pl.TW);
     if (pl.IMGS < 1) pl.IMGS = 1;
   }
-  const int want = pl.IMGS, halo = (pl.TH + 2) * (pl.TW + 2);
+  const int want = pl.IMGS, halo = (pl.TH + 2) * halo_pitch(pl.TW);
   while (pl.IMGS > 1 && pl.IMGS * halo > kWMaxHalo) --pl.IMGS;
   if (pl.IMGS < want) {  // whole small images: pack up to 64 tiles in the big stage
     pl.big = 1;
