@@ -336,14 +336,23 @@ def main():
         return 0
     if world != args.gpus:
         raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE={world}")
+    # IDF_DIST_BACKEND=gloo IDF_SHARE_GPU=1: every rank on cuda:0, collectives staged through
+    # host memory -- a one-GPU rehearsal of the N-rank path (the real run is RCCL, one GPU each)
+    backend = os.environ.get("IDF_DIST_BACKEND", "nccl")
+    if os.environ.get("IDF_SHARE_GPU") == "1":
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
         assert dist.get_world_size() == args.gpus, "process group size != --gpus"
 
     from idfcodec import _lib, configs, synthetic
-    from idfcodec.dist import broadcast_state, gather_bitstream, scatter_bitstream, shard_range
+    from idfcodec.dist import (all_reduce, broadcast_state, gather_bitstream, scatter_bitstream,
+                               shard_range)
 
     cfg = configs.get("imagenet64")
     model = synthetic.build_model(cfg).to(dev)
@@ -389,7 +398,7 @@ def main():
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        all_reduce(t, dist.ReduceOp.MAX)
     elapsed = float(t.item())
     rans = rans_roofline(codec.coder.trace, bs, args.steps)
     codec.coder.trace = None
@@ -400,7 +409,7 @@ def main():
     # single-batch bitstream decoded on rank 0 alone, below)
     ok = torch.tensor([1 if torch.equal(out, img) else 0], dtype=torch.int64, device=dev)
     if world > 1:
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        all_reduce(ok, dist.ReduceOp.MIN)
     exact = bool(ok.item())
     full_exact = None
     if world > 1 and rank == 0:

@@ -95,19 +95,71 @@ def shard_streams(states, nwords, words, n_levels: int, n_images: int, lo: int, 
 
 
 # ------------------------------------------------------------------ collectives
+# Backend "nccl" (RCCL over xGMI) moves device tensors directly.  Backend "gloo" moves host
+# tensors only: there a device tensor is staged through host memory, so the same code runs
+# the bench's N-rank path on one GPU (IDF_DIST_BACKEND=gloo, a rehearsal of the RCCL run).
+def _staged(t, group) -> bool:
+    return t.is_cuda and dist.get_backend(group) == dist.Backend.GLOO
+
+
 def _p2p(ops):
+    """ops: (is_send, tensor, peer, group) tuples or None; runs them as one batch."""
     ops = [o for o in ops if o is not None]
-    if ops:
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
+    if not ops:
+        return
+    p2p, back = [], []
+    for is_send, t, peer, group in ops:
+        if _staged(t, group):
+            h = t.cpu() if is_send else torch.empty(t.shape, dtype=t.dtype)
+            if not is_send:
+                back.append((t, h))
+            t = h
+        p2p.append(dist.P2POp(dist.isend if is_send else dist.irecv, t, peer, group))
+    for req in dist.batch_isend_irecv(p2p):
+        req.wait()
+    for t, h in back:
+        t.copy_(h)
 
 
 def _send(t, peer, group):
-    return dist.P2POp(dist.isend, t, peer, group) if t.numel() else None
+    return (True, t, peer, group) if t.numel() else None
 
 
 def _recv(t, peer, group):
-    return dist.P2POp(dist.irecv, t, peer, group) if t.numel() else None
+    return (False, t, peer, group) if t.numel() else None
+
+
+def _broadcast(t, src, group):
+    if _staged(t, group):
+        h = t.cpu()
+        dist.broadcast(h, src=src, group=group)
+        t.copy_(h)
+    else:
+        dist.broadcast(t, src=src, group=group)
+
+
+def all_reduce(t, op=dist.ReduceOp.SUM, group=None):
+    """dist.all_reduce, staged through host memory under gloo."""
+    if _staged(t, group):
+        h = t.cpu()
+        dist.all_reduce(h, op=op, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op, group=group)
+
+
+def _gather_hdr(hdr, dst, group):
+    """A fixed-size int64 header from every rank to dst: the list of headers on dst, else None."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if _staged(hdr, group):
+        h = hdr.cpu()
+        hs = [torch.empty_like(h) for _ in range(world)] if rank == dst else None
+        dist.gather(h, hs, dst=dst, group=group)
+        return hs
+    hs = [torch.empty_like(hdr) for _ in range(world)] if rank == dst else None
+    dist.gather(hdr, hs, dst=dst, group=group)
+    return hs
 
 
 def gather_streams(states: torch.Tensor, nwords: torch.Tensor, words: torch.Tensor, dst: int = 0,
@@ -117,12 +169,10 @@ def gather_streams(states: torch.Tensor, nwords: torch.Tensor, words: torch.Tens
     Shards may differ in size.  Returns, on `dst`, (states, nwords, words) concatenated in
     rank order; None elsewhere.  Traffic: a 16-byte header per rank through a gather, then
     each shard's metadata and words sent once, point to point, to dst."""
-    world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = words.device
     hdr = torch.tensor([states.numel(), words.numel()], dtype=torch.int64, device=dev)
-    hdrs = [torch.empty_like(hdr) for _ in range(world)] if rank == dst else None
-    dist.gather(hdr, hdrs, dst=dst, group=group)
+    hdrs = _gather_hdr(hdr, dst, group)
     meta = torch.cat([states.view(torch.int64), nwords.to(torch.int64)])
     if rank != dst:
         _p2p([_send(meta, dst, group), _send(words.contiguous(), dst, group)])
@@ -163,7 +213,7 @@ def scatter_streams(states, nwords, words, n_levels: int, n_images: int, src: in
     rank = dist.get_rank(group)
     dev = words.device if rank == src else torch.device(device or "cpu")
     hdr = torch.tensor([n_levels, n_images], dtype=torch.int64, device=dev)
-    dist.broadcast(hdr, src=src, group=group)
+    _broadcast(hdr, src, group)
     n_levels, n_images = (int(v) for v in hdr.cpu().tolist())
     ranges = _rank_counts(n_images, world)
     lo, hi = ranges[rank]
@@ -205,7 +255,7 @@ def broadcast_state(module: torch.nn.Module, src: int = 0, group=None):
         by_dtype.setdefault((t.dtype, t.device), []).append(t)
     for (dt, dv), ts in sorted(by_dtype.items(), key=lambda kv: str(kv[0])):
         flat = torch.cat([t.detach().reshape(-1) for t in ts])
-        dist.broadcast(flat, src=src, group=group)
+        _broadcast(flat, src, group)
         o = 0
         with torch.no_grad():
             for t in ts:
@@ -216,12 +266,10 @@ def broadcast_state(module: torch.nn.Module, src: int = 0, group=None):
 
 def gather_padded(t: torch.Tensor, dst: int = 0, group=None):
     """Gather a variable-length 1-D tensor from every rank to `dst` (rank order); None elsewhere."""
-    world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = t.device
     hdr = torch.tensor([t.numel()], dtype=torch.int64, device=dev)
-    hdrs = [torch.empty_like(hdr) for _ in range(world)] if rank == dst else None
-    dist.gather(hdr, hdrs, dst=dst, group=group)
+    hdrs = _gather_hdr(hdr, dst, group)
     if rank != dst:
         _p2p([_send(t.contiguous(), dst, group)])
         return None
@@ -272,7 +320,7 @@ def agree_conv_mode(bs, group=None):
     from .codec import CONV_CODES
     code = CONV_CODES[bs.meta.get("conv", "f32")]
     both = torch.tensor([code, -code], dtype=torch.int64, device=bs.words.device)
-    dist.all_reduce(both, op=dist.ReduceOp.MAX, group=group)
+    all_reduce(both, dist.ReduceOp.MAX, group)
     hi, neg_lo = both.cpu().tolist()
     if hi != -neg_lo:
         raise ValueError("shards coded with different conv modes: re-encode the x3 shards "
@@ -311,11 +359,11 @@ def scatter_bitstream(bs, src: int = 0, group=None, device=None):
     else:
         dev = torch.device(device or "cpu")
         nlev = torch.empty(1, dtype=torch.int64, device=dev)
-    dist.broadcast(nlev, src=src, group=group)
+    _broadcast(nlev, src, group)
     n_levels = int(nlev.item())
     if rank != src:
         hdr_shapes = torch.empty(3 * n_levels + 2, dtype=torch.int64, device=nlev.device)
-    dist.broadcast(hdr_shapes, src=src, group=group)
+    _broadcast(hdr_shapes, src, group)
     h = hdr_shapes.cpu().tolist()
     shapes = [tuple(h[3 * i: 3 * i + 3]) for i in range(n_levels)]
     sub_per_img, code = h[-2], h[-1]

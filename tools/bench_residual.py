@@ -47,7 +47,7 @@ def run(config: str, batch: int | None = None, steps: int = 2, warmup: int = 1,
     rank = dist.get_rank() if dist.is_initialized() else 0
     dev = torch.device("cuda", torch.cuda.current_device())
     from idfcodec import configs, synthetic
-    from idfcodec.dist import gather_residual
+    from idfcodec.dist import all_reduce, gather_residual
     codec, fl, vq, (H, W) = synthetic.build_residual(config, device=dev, precision=precision)
     pb, pr = configs.PAD.get(config, (0, 0))
     Hs, Ws = H - pb, W - pr
@@ -93,7 +93,7 @@ def run(config: str, batch: int | None = None, steps: int = 2, warmup: int = 1,
     t_idx, t_rec = vq_time()
     if world > 1:
         t = torch.tensor([te, td, t_idx, t_rec, 0.0 if exact else 1.0], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        all_reduce(t, dist.ReduceOp.MAX)
         te, td, t_idx, t_rec = (float(v) for v in t[:4])
         exact = float(t[4]) == 0.0
     res = None
