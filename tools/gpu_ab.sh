@@ -1,24 +1,17 @@
 #!/bin/bash
-# same-box A/B of the wx3 conv: baseline build (tools/native/wino_base_0) vs the working tree
-# (wino_ablate_0), alternated three times.
+# A/B of a bit-identical performance switch: parity tests first, then alternating bench runs.
+# usage: tools/gpu_ab.sh "ENV=0" "ENV=1" [test files...]
 set -u -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
-: > gpurun_out/ab.log
-for r in 1 2 3; do
-  for b in wino_base_0 wino_ablate_0; do
-    echo "== $b" >> gpurun_out/ab.log
-    timeout -k 10 60 ./tools/native/$b x3 >> gpurun_out/ab.log 2>&1 || exit $?
-  done
+export PYTHONDONTWRITEBYTECODE=1
+A=$1; B=$2; shift 2
+if [ $# -gt 0 ]; then
+  timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu "$@" \
+    > gpurun_out/ab_tests.log 2>&1; rc=$?; tail -3 gpurun_out/ab_tests.log; [ $rc -eq 0 ] || exit $rc
+fi
+for v in "$A" "$B" "$A" "$B"; do
+  env $v timeout -k 10 300 python bench.py --no-cpu-baseline --no-residual --steps 10 --warmup 2 \
+    > gpurun_out/ab_b.log 2>&1 || { tail -20 gpurun_out/ab_b.log; exit 1; }
+  echo "$v: $(tail -1 gpurun_out/ab_b.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["encode_ms"], d["decode_ms"], d["round_trip_exact"], d["roofline"]["frac"])')"
 done
-python3 - <<'PY'
-import re, collections
-cur = None; t = collections.defaultdict(list)
-for l in open('gpurun_out/ab.log'):
-    if l.startswith('=='): cur = l.split()[1]; continue
-    m = re.search(r'hw=(\d+) c=(\d+): ([\d.]+) us', l)
-    if m: t[(m.group(1), m.group(2), cur)].append(float(m.group(3)))
-for hw, c in sorted({(k[0], k[1]) for k in t}, key=lambda x: (-int(x[0]), -int(x[1]))):
-    a, b = t[(hw, c, 'wino_base_0')], t[(hw, c, 'wino_ablate_0')]
-    print(f"hw={hw} c={c}: base {min(a):.1f} us  new {min(b):.1f} us  ({100*(min(b)/min(a)-1):+.1f}%)  runs {a} {b}")
-PY
