@@ -265,7 +265,9 @@ def conv_algorithmic_bytes(eng, B):
     n = byt = 0
     for l, L in enumerate(eng.levels):
         P = B * L.h * L.w
-        for geom in [b.geom for b in eng.couple[l]] + [eng.prior[l].geom]:
+        # IDFlows' top prior sees zeros: computed once per model, not per encode
+        cached = L.prior_x_zero and not eng.conditional
+        for geom in [b.geom for b in eng.couple[l]] + ([] if cached else [eng.prior[l].geom]):
             c = geom.a
             for g in geom.growth:
                 n += 1
