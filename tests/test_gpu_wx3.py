@@ -99,7 +99,9 @@ def run_case(B, H, W, C, N, act, fold, scale=1.0, spike=None, res=False, check_i
     (4, 1, 3, 16, 16, "ReLU", True), (2, 9, 9, 100, 44, "ReLU", False),
     (1, 45, 37, 20, 44, "ReLU", True),
     (130, 2, 2, 40, 44, "ReLU", True), (33, 4, 4, 100, 44, "ReLU", True),
-    (17, 3, 3, 24, 32, "LeakyReLU", False)])
+    (17, 3, 3, 24, 32, "LeakyReLU", False),
+    # resflow-patches-vqvae's 27x23 patches (tiled 24 wide): couplings N = 32, prior N = 43
+    (3, 27, 23, 100, 32, "LeakyReLU", True), (2, 27, 23, 200, 43, "LeakyReLU", True)])
 def test_wx3_vs_fp64(B, H, W, C, N, act, fold):
     (e32, ex3), flag = run_case(B, H, W, C, N, act, fold)
     print(f"f32 {e32:.2e} x3 {ex3:.2e}")
@@ -138,3 +140,12 @@ def test_wx3_output_guard_sets_flag():
     assert flag == 1
     _, flag = run_case(1, 8, 8, 16, 16, "None", True, scale=100.0, check_in=0)
     assert flag == 0
+
+
+@pytest.mark.parametrize("B,H,W,C,N", [(3, 27, 23, 100, 32), (2, 27, 23, 200, 43),
+                                       (2, 32, 32, 100, 43), (4, 8, 8, 100, 43)])
+def test_wx3_unchecked_layers(B, H, W, C, N):
+    """The instantiations without the input range check (every DenseLayer after the block's
+    first) at the compile-time tile widths: 24 (two and three n-fragments), 32, 8."""
+    (e32, ex3), flag = run_case(B, H, W, C, N, "LeakyReLU", True, check_in=0)
+    assert flag == 0 and ex3 <= 1e-5 and ex3 <= max(4 * e32, 1e-6), (e32, ex3)
