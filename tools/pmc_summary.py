@@ -11,7 +11,7 @@ def main():
     d = sys.argv[1]
     sub = sys.argv[2] if len(sys.argv) > 2 else ""
     vals = defaultdict(lambda: defaultdict(list))
-    for f in sorted(glob.glob(os.path.join(d, "*.csv"))):
+    for f in sorted(glob.glob(os.path.join(d, "**", "*.csv"), recursive=True)):
         for r in csv.DictReader(open(f)):
             k = r.get("Kernel_Name", "")
             if sub not in k:
