@@ -43,7 +43,8 @@
 // bit 0 skips the per-slab DMA, bit 1 skips the halo LDS reads, bit 2 skips the MFMAs,
 // bit 3 skips the input transform, bit 4 the in-loop barrier, bit 5 the U loads, bit 6
 // makes every halo DMA piece read 1 KiB of contiguous (wrong) memory, bit 8 (256) skips the
-// X3 f16 split, 128 the epilogue's global stores, 1024 its staging reads.
+// X3 f16 split, 128 the epilogue's global stores, 1024 its staging reads, 2048 the vector
+// epilogue's second barrier per n-fragment (races: timing only).
 #ifndef IDF_WINO_ABLATE
 #define IDF_WINO_ABLATE 0
 #endif
@@ -1183,7 +1184,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
         epi_barrier();
         if (IDF_WINO_STAMPS) st_e[1 + 2 * j] = __builtin_amdgcn_s_memtime();
         read_frag(j);
-        epi_barrier();  // the reads landed; every wave is done with the staging
+        if (!(IDF_WINO_ABLATE & 2048)) epi_barrier();  // the reads landed; every wave is done with the staging
         if (IDF_WINO_STAMPS) st_e[2 + 2 * j] = __builtin_amdgcn_s_memtime();
       };
       frag(std::integral_constant<int, 0>{});

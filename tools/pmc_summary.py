@@ -13,6 +13,8 @@ def main():
     vals = defaultdict(lambda: defaultdict(list))
     for f in sorted(glob.glob(os.path.join(d, "**", "*.csv"), recursive=True)):
         for r in csv.DictReader(open(f)):
+            if "Counter_Name" not in r:  # agent-info and other non-counter CSVs
+                break
             k = r.get("Kernel_Name", "")
             if sub not in k:
                 continue
