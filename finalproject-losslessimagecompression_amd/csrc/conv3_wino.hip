@@ -62,6 +62,17 @@
 #ifndef IDF_X3_PRIO
 #define IDF_X3_PRIO 0
 #endif
+// Vector-epilogue variants (same bits, same-box A/B in profiles/r02/ablate/epi_fma_w2/):
+// IDF_EPI_FMA, the output transform's row select as two fmas with a +-1 factor instead of both
+// forms and a per-lane select (on: c=16 launch -2.7%, c=496 -0.3%); IDF_EPI_W2, the staging
+// writes as inline-asm ds_write2_b32 instead of v_mov pairs + ds_write_b64 (off: +9% at c=16
+// -- the asm's memory clobber pins the writes in program order).
+#ifndef IDF_EPI_FMA
+#define IDF_EPI_FMA 1
+#endif
+#ifndef IDF_EPI_W2
+#define IDF_EPI_W2 0
+#endif
 // X3 products: 1 = Vl.Uh (K=16) + (Vh.Uh + Vh.Ul) (one K=32 MFMA), 0 = three K=16 MFMAs.
 // Measured no faster (0.91 vs 0.90 ms over the kbench layers), so off.  Note: hipcc (ROCm
 // 7.2) emits NO wait states between a v_mfma_f32_16x16x32_f16 and a following
@@ -1096,8 +1107,9 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   static_assert(!REGS || 16 * ERW <= BT_OFF, "REGS staging must fit below the bias table");
   if (g.ksplit == 1 && !REGS)
     stage_bias(btab, NF * 16, nf0 * 16, g.N, g.b3, g.vtap, g.bfull, g.ldv, tid, kWThreads);
-  // REGS staging write of n-fragment j: a wave's two positions are adjacent, one 8-B write
-  // per (tile fragment, row)
+  // REGS staging write of n-fragment j: a wave's two positions are adjacent, two dword writes
+  // per (tile fragment, row) that merge into one ds_write2_b32 (an 8-B write needs its values
+  // in an adjacent register pair: two v_mov per write from the accumulators)
   auto write_regs = [&](auto jc) {
     constexpr int j = decltype(jc)::value;
 #pragma unroll
@@ -1105,8 +1117,15 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int t = 16 * i + (lane >> 4) * 4 + r;
-        typedef float f2s __attribute__((ext_vector_type(2)));
-        *(f2s*)(Ms + lr * ERW + t * TPI_ + 2 * wave) = f2s{acc[i][j][r], acc[i][NF + j][r]};
+        if constexpr (IDF_EPI_W2) {
+          // (the epilogue's barriers wait lgkmcnt(0) before any read of the staging)
+          const uint32_t a = (uint32_t)(uintptr_t)(lds_ptr_t)(Ms + lr * ERW + t * TPI_ + 2 * wave);
+          const float x0 = acc[i][j][r], x1 = acc[i][NF + j][r];
+          asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" :: "v"(a), "v"(x0), "v"(x1) : "memory");
+        } else {
+          typedef float f2s __attribute__((ext_vector_type(2)));
+          *(f2s*)(Ms + lr * ERW + t * TPI_ + 2 * wave) = f2s{acc[i][j][r], acc[i][NF + j][r]};
+        }
       }
   };
   if constexpr (REGS) {
@@ -1130,6 +1149,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
           }
         }
       };
+      const float sg = v_r == 0 ? 1.0f : -1.0f;
       auto finish_frag = [&](int j) {
         const int nl = 4 * v_nq, n0 = (nf0 + j) * 16 + nl;
         if (!(v_img < g.IMGS && n0 < g.N)) return;
@@ -1137,10 +1157,14 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const w4 ma = R[k][0], mb = R[k][1], mc = R[k][2];
+          // row 0: (m0 + m1) + m2, row 1: (m1 - m2) - m3, as fma(sg, b, a) with sg = +-1: the
+          // product is exact, so each fma rounds exactly like the add / subtract it replaces
+          // (no per-lane select between both forms)
           float u[4];
 #pragma unroll
           for (int b = 0; b < 4; ++b)
-            u[b] = v_r == 0 ? (ma[b] + mb[b]) + mc[b] : (ma[b] - mb[b]) - mc[b];
+            u[b] = IDF_EPI_FMA ? __builtin_fmaf(sg, mc[b], __builtin_fmaf(sg, mb[b], ma[b]))
+                               : (v_r == 0 ? (ma[b] + mb[b]) + mc[b] : (ma[b] - mb[b]) - mc[b]);
           Y[0][k] = (u[0] + u[1]) + u[2];
           Y[1][k] = (u[1] - u[2]) - u[3];
           if constexpr (X3) {
