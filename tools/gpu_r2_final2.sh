@@ -2,7 +2,7 @@
 # Round-end evidence at the last commit: GPU suite, smoke, bench line, rocprofv3 kernel stats.
 set -u -o pipefail
 cd "$(dirname "$0")/.."
-O=gpurun_out/final2
+O=${O:-gpurun_out/final2}
 mkdir -p $O
 export PYTHONDONTWRITEBYTECODE=1
 timeout -k 10 900 python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests > $O/gpu_tests.log 2>&1; rc=$?
