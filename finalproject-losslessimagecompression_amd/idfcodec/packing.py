@@ -177,9 +177,7 @@ def wino_weights_x3(w: np.ndarray, nslab: int, U: np.ndarray | None = None):
         U = wino_transform64(w, nslab)
     n_alloc = U.shape[1]
     nft = n_alloc // 16
-    m = float(np.abs(U).max())
-    k = 0 if m == 0.0 else int(np.floor(np.log2(16384.0 / m)))
-    k = max(-14, min(k, 60))
+    k = x3_scale(U)
     Us = U * (2.0 ** k)
     hi = Us.astype(np.float16)
     lo = (Us - hi.astype(np.float64)).astype(np.float16)
@@ -188,6 +186,39 @@ def wino_weights_x3(w: np.ndarray, nslab: int, U: np.ndarray | None = None):
     out[..., 1, :] = lo.view(np.uint16).reshape(16, nft, 16, nslab, 4, 4)
     out = out.transpose(0, 3, 1, 4, 2, 5, 6)  # pos, slab, f, h, r, hi/lo, e
     return np.ascontiguousarray(out.reshape(16, nslab, nft, 64, 8)), float(2.0 ** -k)
+
+
+def x3_scale(U: np.ndarray) -> int:
+    """k of the split-f16 pairs: max |U| * 2^k in [2^14, 2^15) (clamped), so the pairs keep full
+    precision down to ~2^-17 of the largest weight."""
+    m = float(np.abs(U).max())
+    k = 0 if m == 0.0 else int(np.floor(np.log2(16384.0 / m)))
+    return max(-14, min(k, 60))
+
+
+def wk_weights(w: np.ndarray, U: np.ndarray | None = None):
+    """Split-f16 Winograd weights for idf_conv3x3_wk (conv3_wk.hip: three K=32 f16 MFMAs per
+    32-channel slab).  U = G g G^T in float64 (wino_transform64, channels zero-padded to a
+    multiple of 32), scaled by 2^k (x3_scale, the same k as wino_weights_x3), split
+    Uh = f16(U'), Ul = f16(U' - Uh).  Returns (uint16 [16 positions][nslab][nft][2: hi, lo]
+    [64 lanes][8], yscale = 2^-k) where lane = 16*q + r holds outputs 16*f + r, channels
+    32*slab + 8*q .. +7 -- the B operand of v_mfma_f32_16x16x32_f16 for k-group q."""
+    if U is None:
+        U = wino_transform64(w, (w.shape[2] + 15) // 16)
+    n_alloc, c16 = U.shape[1], U.shape[2]
+    nft = n_alloc // 16
+    nslab = (c16 + 31) // 32
+    Up = np.zeros((16, n_alloc, nslab * 32), np.float64)
+    Up[:, :, :c16] = U
+    k = x3_scale(Up)
+    Us = Up * (2.0 ** k)
+    hi = Us.astype(np.float16)
+    lo = (Us - hi.astype(np.float64)).astype(np.float16)
+    out = np.empty((16, nslab, nft, 2, 4, 16, 8), np.uint16)  # pos, slab, f, hi/lo, q, r, e
+    for t, part in enumerate((hi, lo)):
+        p = part.view(np.uint16).reshape(16, nft, 16, nslab, 4, 8)  # pos, f, r, slab, q, e
+        out[:, :, :, t] = p.transpose(0, 3, 1, 4, 2, 5)
+    return np.ascontiguousarray(out.reshape(16, nslab, nft, 2, 64, 8)), float(2.0 ** -k)
 
 
 def bf16_weights(w: np.ndarray, C: int) -> np.ndarray:

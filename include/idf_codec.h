@@ -305,6 +305,30 @@ int idf_conv3x3_wx3_res(void *stream, int32_t B, int32_t H, int32_t W, int32_t C
                         float slope, uint32_t *d_flag, int32_t check_input,
                         float *d_workspace, int64_t workspace_floats);
 
+/* "wk": the same split-f16 Winograd convs (same products, same 1e-5 contract, same range
+ * guard and arguments as idf_conv3x3_wx3 / _wx3_res) with all three products on K=32 MFMAs
+ * (v_mfma_f32_16x16x32_f16, 32-channel slabs, one wave per SIMD; conv3_wk.hip).  d_u: uint16
+ * [16 positions][ceil(C/32) slabs][nft][hi, lo][64 lanes][8] (idfcodec/packing.py wk_weights).
+ * Replaces the reference's DenseLayer conv (nnlayer.py:48-51, 1x1 folded in) and the VQ-VAE
+ * 3x3 convs (nnblock.py:59-84).  Every geometry idf_conv3x3_wino_supported takes except the
+ * packed-small-image stage (idf_conv3x3_wk_supported: 4x4 / 2x2 images stay on wx3); the
+ * outputs differ from wx3's in the last bits (another fixed summation order), so an encoder
+ * and its decoder must run the same one. */
+int idf_conv3x3_wk_supported(int32_t H, int32_t W);
+int64_t idf_conv3x3_wk_workspace(int32_t B, int32_t H, int32_t W, int32_t C, int32_t N);
+int idf_conv3x3_wk(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, const float *d_x,
+                   int64_t ld_x, const uint16_t *d_u, int32_t nft, float yscale,
+                   const float *d_b3, const float *d_vtap, int32_t ldv, const float *d_bfull,
+                   int32_t N, float *d_out, int64_t ld_out, int32_t act, float slope,
+                   uint32_t *d_flag, int32_t check_input, float *d_workspace,
+                   int64_t workspace_floats);
+int idf_conv3x3_wk_res(void *stream, int32_t B, int32_t H, int32_t W, int32_t C,
+                       const float *d_x, int64_t ld_x, const uint16_t *d_u, int32_t nft,
+                       float yscale, const float *d_bias, int32_t N, float *d_out,
+                       int64_t ld_out, const float *d_res, int64_t ld_res, int32_t act,
+                       float slope, uint32_t *d_flag, int32_t check_input,
+                       float *d_workspace, int64_t workspace_floats);
+
 /* The same folded 3x3 conv on bf16 MFMA (v_mfma_f32_16x16x32_bf16, fp32 accumulation).
  * The input is the bf16 shadow d_x16 of the fp32 feature columns (ld_x16 a multiple of 8,
  * 16-B aligned; channels [C, round_up(C, 8)) must hold zeros) -- halos are DMA'd straight
