@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "idf_cdf.h"
@@ -423,6 +424,24 @@ __global__ void __launch_bounds__(256) log_prob_kernel(int64_t group_len,
   if (threadIdx.x == 0 && gsum) gsum[blockIdx.x] = red[0];
 }
 
+// Per-element logP only (no group sums): one element per thread over a grid-stride loop,
+// the same arithmetic as log_prob_kernel so both paths agree bit for bit.
+__global__ void __launch_bounds__(256) log_prob_elem_kernel(int64_t n, const float* __restrict__ x,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ logscale,
+                                                            float half_bin, float eps,
+                                                            float* __restrict__ logp) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+    const float sc = expf(logscale[k]);
+    const float xm = x[k], mu = mean[k];
+    const float xp = ((xm + half_bin) - mu) / sc;
+    const float xn = ((xm - half_bin) - mu) / sc;
+    const float lp = idf_logsigmoid(xp), ln = idf_logsigmoid(xn);
+    logp[k] = lp + logf((1.0f - expf(ln - lp)) + eps);
+  }
+}
+
 __global__ void quant_u8_kernel(int B, int C, int H, int W, const float* __restrict__ in, int64_t ld,
                                 uint8_t* __restrict__ img, int32_t* __restrict__ bad) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -735,6 +754,15 @@ int idf_log_prob(void* stream, int64_t n_groups, int64_t group_len, const float*
   if (n_groups == 0) return IDF_OK;
   if (n_groups > 0x7fffffff || !x || !mean || !logscale) return IDF_ERR_ARG;
   const float half_bin = 0.5f / (float)(1 << nbits);
+  if (!group_sum) {
+    if (!logp) return IDF_OK;
+    const int64_t n = n_groups * group_len;
+    if (n == 0) return IDF_OK;
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(log_prob_elem_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                       (hipStream_t)stream, n, x, mean, logscale, half_bin, eps, logp);
+    return idf_last_error();
+  }
   hipLaunchKernelGGL(log_prob_kernel, dim3((unsigned)n_groups), dim3(256), 0,
                      (hipStream_t)stream, group_len, x, mean, logscale, half_bin, eps, logp,
                      group_sum);

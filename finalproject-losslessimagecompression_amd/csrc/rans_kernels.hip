@@ -29,6 +29,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "idf_cdf.h"
 #include "idf_codec_internal.h"
 
@@ -910,101 +912,187 @@ int idf_expf_checksum(void* stream, uint64_t lo, uint64_t hi, unsigned long long
 }
 
 // ---- host-buffer convenience: exactly one reference call (rans.pyx:37 / :69)
+// The _on forms run on the caller's stream with the caller's device workspace
+// (idf_rans_host_workspace_bytes): async copies in, the batched kernels, async copies out, then
+// a sync of that stream only (the outputs are host buffers).  The plain forms keep the
+// reference's signature and run the same on a per-thread non-blocking stream with a per-thread
+// workspace that only grows (no allocation per call, no device-wide sync); both are
+// deliberately kept until the process exits.
+namespace {
+struct HostCarve {
+  char* p;
+  char* end;
+  char* take(size_t b) {
+    char* r = p;
+    p += (b + 255) & ~(size_t)255;
+    return p <= end ? r : nullptr;
+  }
+};
+struct HostCtx {
+  hipStream_t stream = nullptr;
+  void* ws = nullptr;
+  int64_t ws_bytes = 0;
+};
+int host_ctx(int64_t need, HostCtx** out) {
+  thread_local HostCtx ctx;
+  if (!ctx.stream && hipStreamCreateWithFlags(&ctx.stream, hipStreamNonBlocking) != hipSuccess) {
+    ctx.stream = nullptr;
+    return IDF_ERR_HIP;
+  }
+  if (need > ctx.ws_bytes) {
+    if (ctx.ws) (void)hipFree(ctx.ws);
+    ctx.ws = nullptr;
+    ctx.ws_bytes = 0;
+    const int64_t grow = std::max<int64_t>(need, 1 << 20);
+    if (hipMalloc(&ctx.ws, (size_t)grow) != hipSuccess) return IDF_ERR_HIP;
+    ctx.ws_bytes = grow;
+  }
+  *out = &ctx;
+  return IDF_OK;
+}
+inline int64_t carve(int64_t b) { return (b + 255) & ~(int64_t)255; }
+}  // namespace
+
 #define CK(expr)                                   \
   do {                                             \
     if ((expr) != hipSuccess && rc == IDF_OK) rc = IDF_ERR_HIP; \
   } while (0)
-int idf_rans_encode(uint64_t* state_io, int64_t n, const float* x, const float* mean,
-                    const float* scale, uint32_t* words, int64_t* nwords_out, int32_t* status_out) {
-  if (n < 0 || !state_io) return IDF_ERR_ARG;
-  hipStream_t s = nullptr;
-  int64_t nn = n > 0 ? n : 1;
+
+int64_t idf_rans_host_workspace_bytes(int64_t n, int64_t nwords) {
+  if (n < 0 || nwords < 0) return -1;
+  const int64_t nn = n > 0 ? n : 1, nwn = nwords > 0 ? nwords : 1;
+  // encode: x, mean, scale, words (<= n), offsets, states, counts, status, kernel workspace
+  const int64_t enc = 4 * carve(nn * 4) + 6 * carve(16) + carve(idf_rans_encode_workspace_bytes(n));
+  // decode: mean, scale, out, words, offsets, states, counts, status, kernel workspace
+  const int64_t dec = 3 * carve(nn * 4) + carve(nwn * 4) + 7 * carve(16) +
+                      carve(idf_rans_decode_workspace_bytes(n));
+  return std::max(enc, dec);
+}
+
+int idf_rans_encode_on(void* stream, void* d_workspace, int64_t workspace_bytes,
+                       uint64_t* state_io, int64_t n, const float* x, const float* mean,
+                       const float* scale, uint32_t* words, int64_t* nwords_out,
+                       int32_t* status_out) {
+  if (n < 0 || !state_io || !d_workspace || (n > 0 && (!x || !mean || !scale || !words)))
+    return IDF_ERR_ARG;
+  if (workspace_bytes < idf_rans_host_workspace_bytes(n, 0)) return IDF_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t nn = n > 0 ? n : 1;
+  HostCarve c{(char*)d_workspace, (char*)d_workspace + workspace_bytes};
+  float* dx = (float*)c.take(nn * 4);
+  float* dm = (float*)c.take(nn * 4);
+  float* ds = (float*)c.take(nn * 4);
+  uint32_t* dw = (uint32_t*)c.take(nn * 4);
+  int64_t* doff = (int64_t*)c.take(16);
+  uint64_t* dst = (uint64_t*)c.take(8);
+  uint64_t* dfs = (uint64_t*)c.take(8);
+  int64_t* dnw = (int64_t*)c.take(8);
+  int32_t* dstat = (int32_t*)c.take(4);
+  (void)c.take(8);
+  void* kws = c.take((size_t)idf_rans_encode_workspace_bytes(n));
+  if (!kws) return IDF_ERR_ARG;
   int rc = IDF_OK;
-  char* dbuf = nullptr;
-  size_t bytes = 3 * nn * 4 + 2 * 8 + 8 + 8 + 8 + 4 + nn * 4 + (size_t)idf_rans_encode_workspace_bytes(n) + 64;
-  if (hipMalloc(&dbuf, bytes) != hipSuccess) return IDF_ERR_HIP;
-  char* p = dbuf;
-  auto take = [&](size_t b) { char* r = p; p += (b + 15) & ~(size_t)15; return r; };
-  float* dx = (float*)take(nn * 4);
-  float* dm = (float*)take(nn * 4);
-  float* ds = (float*)take(nn * 4);
-  int64_t* doff = (int64_t*)take(16);
-  uint64_t* dst = (uint64_t*)take(8);
-  uint64_t* dfs = (uint64_t*)take(8);
-  int64_t* dnw = (int64_t*)take(8);
-  int32_t* dstat = (int32_t*)take(4);
-  uint32_t* dw = (uint32_t*)take(nn * 4);
-  void* ws = take((size_t)idf_rans_encode_workspace_bytes(n));
-  int64_t off[2] = {0, n};
+  const int64_t off[2] = {0, n};
   if (n > 0) {
-    CK(hipMemcpy(dx, x, n * 4, hipMemcpyHostToDevice));
-    CK(hipMemcpy(dm, mean, n * 4, hipMemcpyHostToDevice));
-    CK(hipMemcpy(ds, scale, n * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpyAsync(dx, x, n * 4, hipMemcpyHostToDevice, s));
+    CK(hipMemcpyAsync(dm, mean, n * 4, hipMemcpyHostToDevice, s));
+    CK(hipMemcpyAsync(ds, scale, n * 4, hipMemcpyHostToDevice, s));
   }
-  CK(hipMemcpy(doff, off, 16, hipMemcpyHostToDevice));
-  CK(hipMemcpy(dst, state_io, 8, hipMemcpyHostToDevice));
+  CK(hipMemcpyAsync(doff, off, 16, hipMemcpyHostToDevice, s));
+  CK(hipMemcpyAsync(dst, state_io, 8, hipMemcpyHostToDevice, s));
   if (rc == IDF_OK)
-    rc = idf_rans_encode_streams(s, 1, n, doff, dx, dm, ds, dst, dfs, dw, dnw, dstat, ws,
-                               idf_rans_encode_workspace_bytes(n));
+    rc = idf_rans_encode_streams(s, 1, n, doff, dx, dm, ds, dst, dfs, dw, dnw, dstat, kws,
+                                 idf_rans_encode_workspace_bytes(n));
   int64_t nw = 0;
   int32_t stat = 0;
+  uint64_t fs = 0;
   if (rc == IDF_OK) {
-    CK(hipMemcpy(state_io, dfs, 8, hipMemcpyDeviceToHost));
-    CK(hipMemcpy(&nw, dnw, 8, hipMemcpyDeviceToHost));
-    CK(hipMemcpy(&stat, dstat, 4, hipMemcpyDeviceToHost));
-    if (nw > 0) CK(hipMemcpy(words, dw, nw * 4, hipMemcpyDeviceToHost));
-    if (hipDeviceSynchronize() != hipSuccess) rc = IDF_ERR_HIP;
+    CK(hipMemcpyAsync(&fs, dfs, 8, hipMemcpyDeviceToHost, s));
+    CK(hipMemcpyAsync(&nw, dnw, 8, hipMemcpyDeviceToHost, s));
+    CK(hipMemcpyAsync(&stat, dstat, 4, hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    if (rc == IDF_OK && nw > 0) {  // the count sizes the last copy
+      CK(hipMemcpyAsync(words, dw, nw * 4, hipMemcpyDeviceToHost, s));
+      CK(hipStreamSynchronize(s));
+    }
+  } else {
+    (void)hipStreamSynchronize(s);  // inputs may still be in flight from the caller's buffers
   }
-  CK(hipFree(dbuf));
+  if (rc == IDF_OK) *state_io = fs;
   if (nwords_out) *nwords_out = nw;
   if (status_out) *status_out = stat;
   return rc;
 }
 
+int idf_rans_decode_on(void* stream, void* d_workspace, int64_t workspace_bytes,
+                       uint64_t* state_io, const uint32_t* words, int64_t nwords, int64_t n,
+                       const float* mean, const float* scale, float* out, int32_t* status_out) {
+  if (n < 0 || nwords < 0 || !state_io || !d_workspace || (nwords > 0 && !words) ||
+      (n > 0 && (!mean || !scale || !out)))
+    return IDF_ERR_ARG;
+  if (workspace_bytes < idf_rans_host_workspace_bytes(n, nwords)) return IDF_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t nn = n > 0 ? n : 1, nwn = nwords > 0 ? nwords : 1;
+  HostCarve c{(char*)d_workspace, (char*)d_workspace + workspace_bytes};
+  float* dm = (float*)c.take(nn * 4);
+  float* ds = (float*)c.take(nn * 4);
+  float* dout = (float*)c.take(nn * 4);
+  uint32_t* dw = (uint32_t*)c.take(nwn * 4);
+  int64_t* doff = (int64_t*)c.take(16);
+  int64_t* dhdr = (int64_t*)c.take(16);  // word offset 0, word count
+  uint64_t* dst = (uint64_t*)c.take(8);
+  uint64_t* dfs = (uint64_t*)c.take(8);
+  int32_t* dstat = (int32_t*)c.take(4);
+  (void)c.take(8);
+  (void)c.take(8);
+  void* kws = c.take((size_t)idf_rans_decode_workspace_bytes(n));
+  if (!kws) return IDF_ERR_ARG;
+  int rc = IDF_OK;
+  const int64_t off[2] = {0, n}, hdr[2] = {0, nwords};
+  if (n > 0) {
+    CK(hipMemcpyAsync(dm, mean, n * 4, hipMemcpyHostToDevice, s));
+    CK(hipMemcpyAsync(ds, scale, n * 4, hipMemcpyHostToDevice, s));
+  }
+  if (nwords > 0) CK(hipMemcpyAsync(dw, words, nwords * 4, hipMemcpyHostToDevice, s));
+  CK(hipMemcpyAsync(doff, off, 16, hipMemcpyHostToDevice, s));
+  CK(hipMemcpyAsync(dhdr, hdr, 16, hipMemcpyHostToDevice, s));
+  CK(hipMemcpyAsync(dst, state_io, 8, hipMemcpyHostToDevice, s));
+  if (rc == IDF_OK)
+    rc = idf_rans_decode_streams(s, 1, n, doff, dhdr, dhdr + 1, dw, dm, ds, dst, dfs, dout,
+                                 dstat, kws, idf_rans_decode_workspace_bytes(n));
+  int32_t stat = 0;
+  uint64_t fs = 0;
+  if (rc == IDF_OK) {
+    CK(hipMemcpyAsync(&fs, dfs, 8, hipMemcpyDeviceToHost, s));
+    CK(hipMemcpyAsync(&stat, dstat, 4, hipMemcpyDeviceToHost, s));
+    if (n > 0) CK(hipMemcpyAsync(out, dout, n * 4, hipMemcpyDeviceToHost, s));
+  }
+  CK(hipStreamSynchronize(s));
+  if (rc == IDF_OK) *state_io = fs;
+  if (status_out) *status_out = stat;
+  return rc;
+}
+
+int idf_rans_encode(uint64_t* state_io, int64_t n, const float* x, const float* mean,
+                    const float* scale, uint32_t* words, int64_t* nwords_out, int32_t* status_out) {
+  if (n < 0 || !state_io) return IDF_ERR_ARG;
+  HostCtx* ctx = nullptr;
+  const int64_t need = idf_rans_host_workspace_bytes(n, 0);
+  int rc = host_ctx(need, &ctx);
+  if (rc != IDF_OK) return rc;
+  return idf_rans_encode_on(ctx->stream, ctx->ws, ctx->ws_bytes, state_io, n, x, mean, scale,
+                            words, nwords_out, status_out);
+}
+
 int idf_rans_decode(uint64_t* state_io, const uint32_t* words, int64_t nwords, int64_t n,
                     const float* mean, const float* scale, float* out, int32_t* status_out) {
   if (n < 0 || nwords < 0 || !state_io) return IDF_ERR_ARG;
-  int64_t nn = n > 0 ? n : 1, nwn = nwords > 0 ? nwords : 1;
-  int rc = IDF_OK;
-  char* dbuf = nullptr;
-  size_t bytes = 3 * nn * 4 + nwn * 4 + 16 + 8 * 4 + 4 + 256 + (size_t)idf_rans_decode_workspace_bytes(n);
-  if (hipMalloc(&dbuf, bytes) != hipSuccess) return IDF_ERR_HIP;
-  char* p = dbuf;
-  auto take = [&](size_t b) { char* r = p; p += (b + 15) & ~(size_t)15; return r; };
-  float* dm = (float*)take(nn * 4);
-  float* ds = (float*)take(nn * 4);
-  float* dout = (float*)take(nn * 4);
-  uint32_t* dw = (uint32_t*)take(nwn * 4);
-  int64_t* doff = (int64_t*)take(16);
-  int64_t* dwoff = (int64_t*)take(8);
-  int64_t* dnw = (int64_t*)take(8);
-  uint64_t* dst = (uint64_t*)take(8);
-  uint64_t* dfs = (uint64_t*)take(8);
-  int32_t* dstat = (int32_t*)take(4);
-  void* dws = take((size_t)idf_rans_decode_workspace_bytes(n));
-  int64_t off[2] = {0, n}, zero = 0;
-  if (n > 0) {
-    CK(hipMemcpy(dm, mean, n * 4, hipMemcpyHostToDevice));
-    CK(hipMemcpy(ds, scale, n * 4, hipMemcpyHostToDevice));
-  }
-  if (nwords > 0) CK(hipMemcpy(dw, words, nwords * 4, hipMemcpyHostToDevice));
-  CK(hipMemcpy(doff, off, 16, hipMemcpyHostToDevice));
-  CK(hipMemcpy(dwoff, &zero, 8, hipMemcpyHostToDevice));
-  CK(hipMemcpy(dnw, &nwords, 8, hipMemcpyHostToDevice));
-  CK(hipMemcpy(dst, state_io, 8, hipMemcpyHostToDevice));
-  if (rc == IDF_OK)
-    rc = idf_rans_decode_streams(nullptr, 1, n, doff, dwoff, dnw, dw, dm, ds, dst, dfs, dout, dstat, dws,
-                                 idf_rans_decode_workspace_bytes(n));
-  int32_t stat = 0;
-  if (rc == IDF_OK) {
-    CK(hipMemcpy(state_io, dfs, 8, hipMemcpyDeviceToHost));
-    CK(hipMemcpy(&stat, dstat, 4, hipMemcpyDeviceToHost));
-    if (n > 0) CK(hipMemcpy(out, dout, n * 4, hipMemcpyDeviceToHost));
-    if (hipDeviceSynchronize() != hipSuccess) rc = IDF_ERR_HIP;
-  }
-  CK(hipFree(dbuf));
-  if (status_out) *status_out = stat;
-  return rc;
+  HostCtx* ctx = nullptr;
+  const int64_t need = idf_rans_host_workspace_bytes(n, nwords);
+  int rc = host_ctx(need, &ctx);
+  if (rc != IDF_OK) return rc;
+  return idf_rans_decode_on(ctx->stream, ctx->ws, ctx->ws_bytes, state_io, words, nwords, n,
+                            mean, scale, out, status_out);
 }
 
 }  // extern "C"

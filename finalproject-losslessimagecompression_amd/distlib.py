@@ -22,20 +22,41 @@ class Distribution(nn.Module):
         super().__init__()
 
 
-def dlogistic_log_prob(x, mean, logscale, nbits=8, eps=1e-8, groups=1, logp=None):
-    """idf_log_prob over contiguous fp32 device tensors split into `groups` equal groups:
-    fills `logp` (if given) and returns the per-group f64 sums (fixed-order reduction)."""
+def dlogistic_log_prob(x, mean, logscale, nbits=8, eps=1e-8, groups=1, logp=None, sums=True):
+    """idf_log_prob over device tensors of x's element count, split into `groups` equal groups:
+    fills `logp` (if given) and returns the per-group f64 sums (fixed-order reduction), or None
+    with sums=False (then one grid-stride elementwise launch fills logp).  mean / logscale are
+    moved to x's device as contiguous fp32 and must have exactly x.numel() elements (broadcast
+    them first); logp must be a contiguous fp32 device tensor of that size."""
     from idfcodec import _lib
     from idfcodec._lib import check, lib, ptr
-    x, mean, logscale = (t.contiguous().float() for t in (x, mean, logscale))
+    require_device(x, "log_prob input")
     n = x.numel()
-    if n % max(groups, 1):
+    x = x.contiguous().float()
+    mean, logscale = (t.to(device=x.device, dtype=torch.float32).contiguous()
+                      if isinstance(t, torch.Tensor) else
+                      torch.as_tensor(t, dtype=torch.float32, device=x.device)
+                      for t in (mean, logscale))
+    for name, t in (("mean", mean), ("logscale", logscale)):
+        if t.numel() != n:
+            raise ValueError(f"log_prob {name} has {t.numel()} elements, x has {n}: "
+                             "broadcast the parameters to x's shape first")
+    if logp is not None:
+        if (logp.device != x.device or logp.dtype != torch.float32 or not logp.is_contiguous()
+                or logp.numel() != n):
+            raise ValueError("log_prob output must be a contiguous fp32 tensor on x's device "
+                             "with x.numel() elements")
+    groups = max(int(groups), 1)
+    if n % groups:
         raise ValueError("log_prob groups must divide the element count")
-    sums = torch.empty(groups, dtype=torch.float64, device=x.device)
-    check(lib().idf_log_prob(_lib.stream_ptr(x.device), groups, n // max(groups, 1), ptr(x),
+    if not sums and logp is None:
+        raise ValueError("log_prob with sums=False needs an output tensor")
+    out = torch.empty(groups, dtype=torch.float64, device=x.device) if sums else None
+    check(lib().idf_log_prob(_lib.stream_ptr(x.device), groups, n // groups, ptr(x),
                              ptr(mean), ptr(logscale), int(nbits), float(eps),
-                             ptr(logp) if logp is not None else None, ptr(sums)), "log_prob")
-    return sums
+                             ptr(logp) if logp is not None else None,
+                             ptr(out) if out is not None else None), "log_prob")
+    return out
 
 
 @NNDistribution.register
@@ -52,9 +73,12 @@ class DLogistic(Distribution):
         """distlib.py:40-55 on the device (idf_log_prob): elementwise, broadcasting as the
         reference's torch ops do."""
         require_device(x, "DLogistic input")
+        mean, logscale = (t.to(x.device) if isinstance(t, torch.Tensor) else
+                          torch.as_tensor(t, dtype=torch.float32, device=x.device)
+                          for t in (mean, logscale))
         x, mean, logscale = torch.broadcast_tensors(x, mean, logscale)
         out = torch.empty(x.shape, dtype=torch.float32, device=x.device)
-        dlogistic_log_prob(x, mean, logscale, nbits, eps, logp=out)
+        dlogistic_log_prob(x, mean, logscale, nbits, eps, logp=out, sums=False)
         return out
 
     def sample(self, mean, logscale, nbits=8):

@@ -158,7 +158,8 @@ class IDFlows(nn.Module):
         total = torch.zeros(B, dtype=torch.float64, device=dev)
         log_Ps = []
         for z, m, ls in zip(latents, means, logscales):
-            sums = dlogistic_log_prob(z.to(dev), m.to(dev), ls.to(dev), self.nbits, groups=B)
+            z, m, ls = torch.broadcast_tensors(z.to(dev), m.to(dev), ls.to(dev))
+            sums = dlogistic_log_prob(z, m, ls, self.nbits, groups=B)
             log_Ps.append((sums / (z.numel() // B)).float())
             total += sums
         return (total / (self.H * self.W * self.C)).float(), log_Ps

@@ -74,6 +74,9 @@ SIGNATURES = {
     "idf_rans_decode_workspace_bytes": (i64, [i64]),
     "idf_rans_decode_streams": (ctypes.c_int, [P, i64, i64, P, P, P, P, P, P, P, P, P, P, P, i64]),
     "idf_gather_words": (ctypes.c_int, [P, i64, P, P, P, P, P]),
+    "idf_rans_host_workspace_bytes": (i64, [i64, i64]),
+    "idf_rans_encode_on": (ctypes.c_int, [P, P, i64, P, i64, P, P, P, P, P, P]),
+    "idf_rans_decode_on": (ctypes.c_int, [P, P, i64, P, P, i64, i64, P, P, P, P]),
     "idf_rans_encode": (ctypes.c_int, [P, i64, P, P, P, P, P, P]),
     "idf_rans_decode": (ctypes.c_int, [P, P, i64, i64, P, P, P, P]),
     "idf_log_prob": (ctypes.c_int, [P, i64, i64, P, P, P, i32, f32, P, P]),

@@ -25,10 +25,12 @@ from ._lib import check, lib, ptr
 
 RANS_L = 1 << 32
 MAGIC = b"IDFB"
-VERSION = 1
+VERSION = 2         # 2: flags always carry the conv arithmetic; version-1 files still read
 FLAG_CONV_X3 = 1
 # container flags bits 0-3: the conv arithmetic the flow ran (engine.conv_family); the decoder
-# must run the same one.  0 = exact-f32 Winograd (every stream written before the field existed)
+# must run the same one.  Version 1 wrote 0 both for exact-f32 Winograd and for every engine
+# that predates the field (halo / gemm / unfold / bf16): a version-1 file with flags 0 reads as
+# conv "unrecorded", which any engine but a split-f16 one may decode (the pre-field behaviour).
 CONV_CODES = {"f32": 0, "x3": 1, "halo": 2, "gemm": 3, "unfold": 4, "bf16": 5}
 CONV_NAMES = {v: k for k, v in CONV_CODES.items()}
 
@@ -44,6 +46,15 @@ class Bitstream:
     words: torch.Tensor           # int32 view of u32 words, stream-major, push order
     status: torch.Tensor | None = None
     meta: dict = field(default_factory=dict)
+    # host (CPU int64) copy of nwords when the producer already had one (encode's compaction,
+    # from_bytes, the multi-GPU exchanges): sizes and checks then never wait on the device
+    host_nwords: torch.Tensor | None = None
+
+    def nwords_host(self) -> torch.Tensor:
+        """nwords on the host: the kept copy, else one device->host read (cached)."""
+        if self.host_nwords is None:
+            self.host_nwords = self.nwords.detach().to("cpu", torch.int64)
+        return self.host_nwords
 
     @property
     def n_streams(self) -> int:
@@ -76,7 +87,9 @@ class Bitstream:
         # 0: exact-f32 (every stream written before the flag existed)
         conv = self.meta.get("conv", "f32")
         if conv not in CONV_CODES:
-            raise ValueError(f"unknown conv mode {conv!r}")
+            raise ValueError(f"unknown conv mode {conv!r}"
+                             + (": a version-1 file without the conv field cannot be rewritten"
+                                " as version 2; re-encode it" if conv == "unrecorded" else ""))
         flags = CONV_CODES[conv]
         hdr = struct.pack("<4sHHIII", MAGIC, VERSION, flags, self.n_images, len(self.level_shapes),
                           self.n_streams)
@@ -90,7 +103,7 @@ class Bitstream:
     @classmethod
     def from_bytes(cls, buf: bytes, device=None) -> "Bitstream":
         magic, ver, flags, n_img, n_lvl, n_str = struct.unpack_from("<4sHHIII", buf, 0)
-        if magic != MAGIC or ver != VERSION:
+        if magic != MAGIC or ver not in (1, VERSION):
             raise ValueError("not an IDF bitstream")
         o = struct.calcsize("<4sHHIII")
         shapes = [struct.unpack_from("<III", buf, o + 12 * i) for i in range(n_lvl)]
@@ -105,8 +118,10 @@ class Bitstream:
         t = lambda a: torch.from_numpy(a).to(device) if device else torch.from_numpy(a)  # noqa: E731
         if (flags & 0xF) not in CONV_NAMES or flags >> 4:
             raise ValueError(f"unknown bitstream flags {flags:#x}")
+        conv = "unrecorded" if ver == 1 and flags == 0 else CONV_NAMES[flags & 0xF]
         return cls(n_img, [tuple(s) for s in shapes], t(st), t(nw), t(w),
-                   meta={"n_subpixels": int(nsub), "conv": CONV_NAMES[flags & 0xF]})
+                   meta={"n_subpixels": int(nsub), "conv": conv},
+                   host_nwords=torch.from_numpy(nw))
 
 
 class StreamCoder:
@@ -170,11 +185,13 @@ class StreamCoder:
                              meta=dict(meta, scratch_offsets=off[:-1]))
         dst_off = torch.zeros_like(nwords)
         dst_off[1:] = torch.cumsum(nwords, 0)[:-1]
-        total = int((dst_off[-1] + nwords[-1]).item())
+        nw_host = nwords.to("cpu")  # the one sync: the compacted size
+        total = int(nw_host.sum())
         words = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
         check(lib().idf_gather_words(s, ns, ptr(off), ptr(nwords), ptr(dst_off), ptr(scratch),
                                      ptr(words)), "gather words")
-        return Bitstream(B, shapes, final, nwords, words[:total], status, meta=meta)
+        return Bitstream(B, shapes, final, nwords, words[:total], status, meta=meta,
+                         host_nwords=nw_host)
 
     def level_encoder(self, B: int):
         """Per-level rANS encode overlapped with the flow: forward_pm calls .level(l, ws)
@@ -292,11 +309,13 @@ class _LevelEncoder:
         ns = off.numel() - 1
         dst_off = torch.zeros_like(nwords)
         dst_off[1:] = torch.cumsum(nwords, 0)[:-1]
-        total = int((dst_off[-1] + nwords[-1]).item())
+        nw_host = nwords.to("cpu")  # the one sync: the compacted size
+        total = int(nw_host.sum())
         words = torch.empty(max(total, 1), dtype=torch.int32, device=eng.device)
         check(lib().idf_gather_words(_lib.stream_ptr(eng.device), ns, ptr(off), ptr(nwords),
                                      ptr(dst_off), ptr(scratch), ptr(words)), "gather words")
-        return Bitstream(B, shapes, final, nwords, words[:total], status, meta=meta)
+        return Bitstream(B, shapes, final, nwords, words[:total], status, meta=meta,
+                         host_nwords=nw_host)
 
 
 class ImageCodec:
@@ -427,14 +446,21 @@ class ImageCodec:
                              f"{len(eng.levels)} levels x {bs.n_images} images")
         if bs.nwords.numel() != bs.n_streams:
             raise ValueError("bitstream word-count table does not match its stream count")
-        if bool((bs.nwords < 0).any().item()):
+        nw_host = bs.nwords_host()
+        if bool((nw_host < 0).any()):
             raise ValueError("bitstream has a negative word count")
         if "scratch_offsets" not in bs.meta:
-            total = int(bs.nwords.sum().item()) if bs.n_streams else 0
+            total = int(nw_host.sum()) if bs.n_streams else 0
             if total != bs.words.numel():
                 raise ValueError(f"bitstream word table sums to {total} words, "
                                  f"{bs.words.numel()} present")
         conv, have = bs.meta.get("conv", "f32"), eng.conv_family
+        if conv == "unrecorded":  # version-1 file, flags 0: any engine but split-f16
+            if have == "x3":
+                raise ValueError("bitstream predates the conv field (version 1, flags 0) and "
+                                 "was not coded with split-f16 convs; decode it with "
+                                 "engine.set_conv_mode('f32') or the engine that wrote it")
+            return
         if conv not in CONV_CODES:
             raise ValueError(f"unknown conv mode {conv!r}")
         switchable = conv in ("x3", "f32") and have in ("x3", "f32") and (conv == "f32" or
@@ -449,7 +475,7 @@ class ImageCodec:
         dev = self.engine.device
         if bs.states.device != dev:
             bs = Bitstream(bs.n_images, bs.level_shapes, bs.states.to(dev), bs.nwords.to(dev),
-                           bs.words.to(dev), None, bs.meta)
+                           bs.words.to(dev), None, bs.meta, bs.host_nwords)
         word_off = bs.meta.get("scratch_offsets")
         if word_off is None:
             word_off = bs.word_offsets()
@@ -539,8 +565,10 @@ class ImageCodec:
                         with torch.cuda.stream(streams[i]):
                             try:
                                 next(gens[i])
-                            except StopIteration:
-                                finish(i, off[i], sz[i], eng.workspace(sz[i], i))
+                            except StopIteration as lane_done:
+                                # the lane's own workspace (a fresh cache lookup could hand
+                                # back a different, uninitialised set once the cache evicts)
+                                finish(i, off[i], sz[i], lane_done.value)
                                 live.remove(i)
                 for st in streams:
                     main.wait_stream(st)

@@ -60,44 +60,125 @@ def _rank_counts(n_images: int, world: int):
     return [shard_range(n_images, r, world) for r in range(world)]
 
 
+# index tensors of the reorders, per (kind, shard layout, device): built once per batch shape,
+# not on every step (a bench step re-uses the same world and batch)
+_ORDERS: dict = {}
+
+
+def _order(key, device, build):
+    k = (key, str(device))
+    t = _ORDERS.get(k)
+    if t is None:
+        if len(_ORDERS) >= 64:
+            _ORDERS.clear()
+        t = _ORDERS[k] = torch.tensor(build(), dtype=torch.int64, device=device)
+    return t
+
+
+def _interleave_idx(counts, n_levels):
+    base, bases = 0, []
+    for c in counts:
+        bases.append(base)
+        base += n_levels * c
+    idx = []
+    for l in range(n_levels):
+        for r, c in enumerate(counts):
+            b0 = bases[r] + l * c
+            idx.extend(range(b0, b0 + c))
+    return idx
+
+
+def _to_device(h: torch.Tensor, device) -> torch.Tensor:
+    """A host tensor on `device` without a stream sync (pinned staging, async copy)."""
+    device = torch.device(device)
+    if device.type == "cpu":
+        return h
+    return h.pin_memory().to(device, non_blocking=True)
+
+
+def _interleave(states, nwords, words, world, n_levels, per_rank_images, total=None,
+                host_nwords=None):
+    counts = ([per_rank_images] * world if isinstance(per_rank_images, int)
+              else list(per_rank_images))
+    if len(counts) != world:
+        raise ValueError("per_rank_images must list one image count per rank")
+    if n_levels * sum(counts) != states.numel():
+        raise ValueError(f"{states.numel()} streams gathered, {n_levels * sum(counts)} expected")
+    key = ("interleave", tuple(counts), n_levels)
+    order = _order(key, states.device, lambda: _interleave_idx(counts, n_levels))
+    worder = order if words.device == states.device else _order(
+        key, words.device, lambda: _interleave_idx(counts, n_levels))
+    nw_h = None
+    if host_nwords is not None:
+        nw_h = host_nwords.to(torch.int64)[_order(key, "cpu", lambda: _interleave_idx(
+            counts, n_levels))]
+        if total is None:
+            total = int(nw_h.sum())
+    nw, w = segment_gather(words, nwords, worder, total)
+    return states[order], nw.to(nwords.dtype), w, nw_h
+
+
 def interleave_levels(states, nwords, words, world: int, n_levels: int,
                       per_rank_images: int | list[int], total: int | None = None):
     """Reorder rank-major gathered streams (rank, level, local image) into the single-batch
     order (level, global image) of idfcodec.codec.Bitstream.  per_rank_images: one count for
     equal shards, or the list of each rank's image count."""
-    counts = ([per_rank_images] * world if isinstance(per_rank_images, int)
-              else list(per_rank_images))
-    if len(counts) != world:
-        raise ValueError("per_rank_images must list one image count per rank")
-    base, bases = 0, []
-    for c in counts:
-        bases.append(base)
-        base += n_levels * c
-    if base != states.numel():
-        raise ValueError(f"{states.numel()} streams gathered, {base} expected")
-    idx = []
-    for l in range(n_levels):
-        for r in range(world):
-            b0 = bases[r] + l * counts[r]
-            idx.extend(range(b0, b0 + counts[r]))
-    order = torch.tensor(idx, dtype=torch.int64, device=states.device)
-    nw, w = segment_gather(words, nwords, order.to(words.device), total)
-    return states[order], nw.to(nwords.dtype), w
+    return _interleave(states, nwords, words, world, n_levels, per_rank_images, total)[:3]
+
+
+def _shard_idx(n_levels, n_images, lo, hi):
+    return [l * n_images + b for l in range(n_levels) for b in range(lo, hi)]
+
+
+def _shard(states, nwords, words, n_levels, n_images, lo, hi, host_nwords=None):
+    key = ("shard", n_levels, n_images, lo, hi)
+    build = lambda: _shard_idx(n_levels, n_images, lo, hi)  # noqa: E731
+    order = _order(key, states.device, build)
+    worder = order if words.device == states.device else _order(key, words.device, build)
+    nw_h, total = None, None
+    if host_nwords is not None:
+        nw_h = host_nwords.to(torch.int64)[_order(key, "cpu", build)]
+        total = int(nw_h.sum())
+    nw, w = segment_gather(words, nwords, worder, total)
+    return states[order], nw.to(nwords.dtype), w, nw_h
 
 
 def shard_streams(states, nwords, words, n_levels: int, n_images: int, lo: int, hi: int):
     """The streams of images [lo, hi) of a single-batch bitstream, in the shard's own order
     (level-major, local-image-minor)."""
-    idx = [l * n_images + b for l in range(n_levels) for b in range(lo, hi)]
-    order = torch.tensor(idx, dtype=torch.int64, device=states.device)
-    nw, w = segment_gather(words, nwords, order.to(words.device))
-    return states[order], nw.to(nwords.dtype), w
+    return _shard(states, nwords, words, n_levels, n_images, lo, hi)[:3]
 
 
 # ------------------------------------------------------------------ collectives
 # Backend "nccl" (RCCL over xGMI) moves device tensors directly.  Backend "gloo" moves host
 # tensors only: there a device tensor is staged through host memory, so the same code runs
 # the bench's N-rank path on one GPU (IDF_DIST_BACKEND=gloo, a rehearsal of the RCCL run).
+#
+# Sizes, word-count tables and header fields are host-resident at their producer (tensor
+# shapes, the encoder's compaction, a file), so they travel on a gloo group over the same
+# ranks: no exchange reads a device value back to size its buffers, and the timed step's
+# stream never drains for one.  Only the payload (final states, words) moves over RCCL.
+_HOST_GROUPS: dict = {}
+# tests set this to build the separate gloo group even when `group` is gloo itself, so the
+# RCCL configuration's two-group traffic runs on CPU
+SEPARATE_HOST_GROUP = False
+
+
+def host_group(group=None):
+    """The gloo group over `group`'s ranks that carries host metadata (`group` itself under
+    gloo).  Created on first use; for a sub-group of an RCCL world every rank of the world must
+    call this once, together, before the first exchange (torch.distributed.new_group is
+    collective over the world)."""
+    if dist.get_backend(group) == dist.Backend.GLOO and not SEPARATE_HOST_GROUP:
+        return group
+    key = None if group is None else id(group)
+    g = _HOST_GROUPS.get(key)
+    if g is None:
+        ranks = None if group is None else dist.get_process_group_ranks(group)
+        g = _HOST_GROUPS[key] = dist.new_group(ranks=ranks, backend="gloo")
+    return g
+
+
 def _staged(t, group) -> bool:
     return t.is_cuda and dist.get_backend(group) == dist.Backend.GLOO
 
@@ -149,99 +230,112 @@ def all_reduce(t, op=dist.ReduceOp.SUM, group=None):
 
 
 def _gather_hdr(hdr, dst, group):
-    """A fixed-size int64 header from every rank to dst: the list of headers on dst, else None."""
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    if _staged(hdr, group):
-        h = hdr.cpu()
-        hs = [torch.empty_like(h) for _ in range(world)] if rank == dst else None
-        dist.gather(h, hs, dst=dst, group=group)
-        return hs
-    hs = [torch.empty_like(hdr) for _ in range(world)] if rank == dst else None
-    dist.gather(hdr, hs, dst=dst, group=group)
+    """A fixed-size host int64 header from every rank to dst over the host group: the list of
+    headers on dst, else None."""
+    hg = host_group(group)
+    world = dist.get_world_size(hg)
+    hs = [torch.empty_like(hdr) for _ in range(world)] if dist.get_rank(hg) == dst else None
+    dist.gather(hdr, hs, dst=dst, group=hg)
     return hs
 
 
-def gather_streams(states: torch.Tensor, nwords: torch.Tensor, words: torch.Tensor, dst: int = 0,
-                   group=None):
-    """Gather every rank's (states[int64 n_s], nwords[int64 n_s], words[int32 total]) to `dst`.
-
-    Shards may differ in size.  Returns, on `dst`, (states, nwords, words) concatenated in
-    rank order; None elsewhere.  Traffic: a 16-byte header per rank through a gather, then
-    each shard's metadata and words sent once, point to point, to dst."""
+def _gather(states, nwords, words, dst, group, host_nwords):
     rank = dist.get_rank(group)
+    hg = host_group(group)
     dev = words.device
-    hdr = torch.tensor([states.numel(), words.numel()], dtype=torch.int64, device=dev)
+    nw_h = (nwords.detach().to("cpu", torch.int64) if host_nwords is None
+            else host_nwords.to(torch.int64))
+    hdr = torch.tensor([states.numel(), words.numel()], dtype=torch.int64)
     hdrs = _gather_hdr(hdr, dst, group)
-    meta = torch.cat([states.view(torch.int64), nwords.to(torch.int64)])
     if rank != dst:
-        _p2p([_send(meta, dst, group), _send(words.contiguous(), dst, group)])
+        _p2p([_send(nw_h, dst, hg)])
+        _p2p([_send(states.view(torch.int64).contiguous(), dst, group),
+              _send(words.contiguous(), dst, group)])
         return None
-    sizes = torch.stack(hdrs).cpu().tolist()  # the one host sync: every shard's sizes
+    sizes = torch.stack(hdrs).tolist()  # host values: every shard's stream and word count
     ns_tot = sum(s[0] for s in sizes)
     nw_tot = sum(s[1] for s in sizes)
+    parts, ops = [], []
+    for r, (ns, _) in enumerate(sizes):
+        if r == rank:
+            parts.append(nw_h)
+        else:
+            parts.append(torch.empty(ns, dtype=torch.int64))
+            ops.append(_recv(parts[-1], r, hg))
+    _p2p(ops)
+    nw_host = torch.cat(parts) if parts else torch.zeros(0, dtype=torch.int64)
     st_out = torch.empty(ns_tot, dtype=torch.int64, device=dev)
-    nw_out = torch.empty(ns_tot, dtype=torch.int64, device=dev)
     w_out = torch.empty(nw_tot, dtype=words.dtype, device=dev)
-    metas, ops = [], []
+    ops = []
     so = wo = 0
     for r, (ns, nw) in enumerate(sizes):
         if r == rank:
             st_out[so:so + ns] = states.view(torch.int64)
-            nw_out[so:so + ns] = nwords.to(torch.int64)
             w_out[wo:wo + nw] = words
         else:
-            m = torch.empty(2 * ns, dtype=torch.int64, device=dev)
-            metas.append((m, so, ns))
-            ops += [_recv(m, r, group), _recv(w_out[wo:wo + nw], r, group)]
+            ops += [_recv(st_out[so:so + ns], r, group), _recv(w_out[wo:wo + nw], r, group)]
         so += ns
         wo += nw
     _p2p(ops)
-    for m, so, ns in metas:
-        st_out[so:so + ns] = m[:ns]
-        nw_out[so:so + ns] = m[ns:]
-    return st_out, nw_out, w_out
+    return st_out, _to_device(nw_host, dev), w_out, nw_host
+
+
+def gather_streams(states: torch.Tensor, nwords: torch.Tensor, words: torch.Tensor, dst: int = 0,
+                   group=None, host_nwords: torch.Tensor | None = None):
+    """Gather every rank's (states[int64 n_s], nwords[int64 n_s], words[int32 total]) to `dst`.
+
+    Shards may differ in size.  Returns, on `dst`, (states, nwords, words) concatenated in
+    rank order; None elsewhere.  Traffic: a 16-byte header and the word-count table per rank
+    on the host group, then each shard's final states and words sent once, point to point,
+    to dst.  host_nwords: the host copy of nwords if the caller has one (else one read)."""
+    got = _gather(states, nwords, words, dst, group, host_nwords)
+    return None if got is None else got[:3]
+
+
+def _scatter(states, nwords, words, n_levels, n_images, src, group, device, host_nwords):
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    hg = host_group(group)
+    dev = words.device if rank == src else torch.device(device or "cpu")
+    hdr = torch.tensor([n_levels, n_images], dtype=torch.int64)
+    dist.broadcast(hdr, src=src, group=hg)
+    n_levels, n_images = (int(v) for v in hdr.tolist())
+    ranges = _rank_counts(n_images, world)
+    lo, hi = ranges[rank]
+    if rank == src:
+        nw_all = (nwords.detach().to("cpu", torch.int64) if host_nwords is None
+                  else host_nwords.to(torch.int64))
+        mine, shards = None, []
+        for r, (a, b) in enumerate(ranges):
+            st, nw, w, nw_h = _shard(states, nwords, words, n_levels, n_images, a, b, nw_all)
+            if r == rank:
+                mine = (st, nw.to(torch.int64), w, nw_h)
+            else:
+                shards.append((r, st, w, nw_h))
+        # word-count tables first, on the host group: receivers size their buffers from them
+        _p2p([_send(nw_h, r, hg) for r, _, _, nw_h in shards])
+        _p2p([op for r, st, w, _ in shards
+              for op in (_send(st.view(torch.int64).contiguous(), r, group),
+                         _send(w.contiguous(), r, group))])
+        return (*mine, (lo, hi))
+    ns = n_levels * (hi - lo)
+    nw_h = torch.empty(ns, dtype=torch.int64)
+    _p2p([_recv(nw_h, src, hg)])
+    st = torch.empty(ns, dtype=torch.int64, device=dev)
+    w = torch.empty(int(nw_h.sum()), dtype=torch.int32, device=dev)
+    _p2p([_recv(st, src, group), _recv(w, src, group)])
+    return st, _to_device(nw_h, dev), w, nw_h, (lo, hi)
 
 
 def scatter_streams(states, nwords, words, n_levels: int, n_images: int, src: int = 0,
-                    group=None, device=None):
+                    group=None, device=None, host_nwords: torch.Tensor | None = None):
     """Decode-side mirror of gather_streams: `src` holds a single-batch bitstream of
     n_images images (states / nwords / words; other ranks pass None and their device);
     every rank receives the streams of its image shard shard_range(n_images, rank, world)
     in shard order.  Returns (states, nwords, words, (lo, hi)) on every rank."""
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    dev = words.device if rank == src else torch.device(device or "cpu")
-    hdr = torch.tensor([n_levels, n_images], dtype=torch.int64, device=dev)
-    _broadcast(hdr, src, group)
-    n_levels, n_images = (int(v) for v in hdr.cpu().tolist())
-    ranges = _rank_counts(n_images, world)
-    lo, hi = ranges[rank]
-    if rank == src:
-        mine = None
-        meta_ops, word_ops, keep = [], [], []
-        for r, (a, b) in enumerate(ranges):
-            st, nw, w = shard_streams(states, nwords, words, n_levels, n_images, a, b)
-            if r == rank:
-                mine = (st, nw.to(torch.int64), w)
-                continue
-            meta = torch.cat([st.view(torch.int64), nw.to(torch.int64)])
-            w = w.contiguous()
-            keep += [meta, w]
-            meta_ops.append(_send(meta, r, group))
-            word_ops.append(_send(w, r, group))
-        # metadata first: receivers size their word buffers from it
-        _p2p(meta_ops)
-        _p2p(word_ops)
-        return (*mine, (lo, hi))
-    ns = n_levels * (hi - lo)
-    meta = torch.empty(2 * ns, dtype=torch.int64, device=dev)
-    _p2p([_recv(meta, src, group)])
-    st, nw = meta[:ns].clone(), meta[ns:].clone()
-    total = int(nw.sum().item()) if ns else 0
-    w = torch.empty(total, dtype=torch.int32, device=dev)
-    _p2p([_recv(w, src, group)])
-    return st, nw, w, (lo, hi)
+    st, nw, w, _, rng = _scatter(states, nwords, words, n_levels, n_images, src, group, device,
+                                 host_nwords)
+    return st, nw, w, rng
 
 
 def broadcast_state(module: torch.nn.Module, src: int = 0, group=None):
@@ -268,12 +362,12 @@ def gather_padded(t: torch.Tensor, dst: int = 0, group=None):
     """Gather a variable-length 1-D tensor from every rank to `dst` (rank order); None elsewhere."""
     rank = dist.get_rank(group)
     dev = t.device
-    hdr = torch.tensor([t.numel()], dtype=torch.int64, device=dev)
+    hdr = torch.tensor([t.numel()], dtype=torch.int64)
     hdrs = _gather_hdr(hdr, dst, group)
     if rank != dst:
         _p2p([_send(t.contiguous(), dst, group)])
         return None
-    sizes = torch.cat(hdrs).cpu().tolist()
+    sizes = torch.cat(hdrs).tolist()
     out = torch.empty(sum(sizes), dtype=t.dtype, device=dev)
     ops, o = [], 0
     for r, n in enumerate(sizes):
@@ -301,30 +395,45 @@ def merge_residual(parts):
     return _assemble(parts[0], len(parts), st, nw, w, torch.cat([p.idx_words for p in parts]))
 
 
-def _assemble(first, world, st, nw, w, idx):
+def _assemble(first, world, st, nw, w, idx, nw_host=None):
     from .codec import Bitstream
     from .residual import ResidualBitstream
     fl = first.flow
-    st, nw, w = interleave_levels(st, nw, w, world, len(fl.level_shapes), fl.n_images)
+    st, nw, w, nw_h = _interleave(st, nw, w, world, len(fl.level_shapes), fl.n_images,
+                                  host_nwords=nw_host)
     meta = {k: v for k, v in fl.meta.items() if k in ("n_subpixels", "conv")}
     if "n_subpixels" in meta:
         meta["n_subpixels"] = meta["n_subpixels"] * world
-    flow = Bitstream(fl.n_images * world, fl.level_shapes, st, nw, w, None, meta)
+    flow = Bitstream(fl.n_images * world, fl.level_shapes, st, nw, w, None, meta, nw_h)
     return ResidualBitstream(flow, idx, first.n_images * world, first.image_shape, first.grid,
                              first.embed_num, first.source_hw)
 
 
-def agree_conv_mode(bs, group=None):
-    """Every shard must have run the same conv arithmetic (a tripped split-f16 range guard on
-    one rank re-encodes that shard with exact-f32 convs).  Raises ValueError otherwise."""
+def agree_shards(bs, group=None):
+    """Before any point-to-point traffic, every rank checks -- on the host group, with one
+    MAX all-reduce -- that all shards ran the same conv arithmetic (a tripped split-f16 range
+    guard on one rank re-encodes that shard with exact-f32 convs), hold the same number of
+    images (gather_bitstream / gather_residual need equal shards) and are compacted (a
+    compact=False stream's words sit at scratch offsets, not back to back).  Every rank raises
+    the same ValueError, so none is left blocked in a later exchange."""
     from .codec import CONV_CODES
-    code = CONV_CODES[bs.meta.get("conv", "f32")]
-    both = torch.tensor([code, -code], dtype=torch.int64, device=bs.words.device)
-    all_reduce(both, dist.ReduceOp.MAX, group)
-    hi, neg_lo = both.cpu().tolist()
-    if hi != -neg_lo:
+    code = CONV_CODES.get(bs.meta.get("conv", "f32"), -1)
+    scratch = int("scratch_offsets" in bs.meta)
+    v = torch.tensor([code, -code, bs.n_images, -bs.n_images, scratch], dtype=torch.int64)
+    dist.all_reduce(v, op=dist.ReduceOp.MAX, group=host_group(group))
+    hi, neg_lo, n_hi, neg_n_lo, any_scratch = v.tolist()
+    if any_scratch:
+        raise ValueError("a shard's bitstream is not compacted (encode(compact=False)): "
+                         "gather compacted bitstreams only")
+    if hi != -neg_lo or hi < 0:
         raise ValueError("shards coded with different conv modes: re-encode the x3 shards "
                          "with engine.set_conv_mode('f32') and gather again")
+    if n_hi != -neg_n_lo:
+        raise ValueError("shards hold different image counts: gather_bitstream needs equal "
+                         "shards (gather_streams + interleave_levels take ragged ones)")
+
+
+agree_conv_mode = agree_shards
 
 
 def gather_bitstream(bs, dst: int = 0, group=None):
@@ -332,55 +441,58 @@ def gather_bitstream(bs, dst: int = 0, group=None):
     gather_streams + interleave_levels, the n_subpixels scaled to the whole batch."""
     from .codec import Bitstream
     world = dist.get_world_size(group)
-    agree_conv_mode(bs, group)
-    got = gather_streams(bs.states, bs.nwords, bs.words, dst=dst, group=group)
+    agree_shards(bs, group)
+    got = _gather(bs.states, bs.nwords, bs.words, dst, group, bs.host_nwords)
     if got is None:
         return None
-    st, nw, w = got
-    st, nw, w = interleave_levels(st, nw, w, world, len(bs.level_shapes), bs.n_images,
-                                  total=w.numel())
+    st, nw, w, nw_h = _interleave(*got[:3], world, len(bs.level_shapes), bs.n_images,
+                                  total=got[2].numel(), host_nwords=got[3])
     meta = {k: v for k, v in bs.meta.items() if k in ("n_subpixels", "conv")}
     if "n_subpixels" in meta:
         meta["n_subpixels"] = meta["n_subpixels"] * world
-    return Bitstream(bs.n_images * world, bs.level_shapes, st, nw, w, None, meta)
+    return Bitstream(bs.n_images * world, bs.level_shapes, st, nw, w, None, meta, nw_h)
 
 
 def scatter_bitstream(bs, src: int = 0, group=None, device=None):
     """Each rank's shard of the single-batch Bitstream `bs` held by `src` (others pass None
     and their device): the decode-side mirror of gather_bitstream.  Returns (Bitstream of
-    the rank's images, (lo, hi))."""
-    from .codec import Bitstream
+    the rank's images, (lo, hi)).  The header travels on the host group."""
+    from .codec import CONV_NAMES, Bitstream
     rank = dist.get_rank(group)
+    hg = host_group(group)
     if rank == src:
+        if "scratch_offsets" in bs.meta:
+            raise ValueError("scatter a compacted bitstream (encode(compact=True))")
         hdr_shapes = torch.tensor([v for s in bs.level_shapes for v in s] +
                                   [bs.meta.get("n_subpixels", 0) // max(bs.n_images, 1),
-                                   _conv_code(bs)], dtype=torch.int64, device=bs.words.device)
-        nlev = torch.tensor([len(bs.level_shapes)], dtype=torch.int64, device=bs.words.device)
+                                   _conv_code(bs)], dtype=torch.int64)
+        nlev = torch.tensor([len(bs.level_shapes)], dtype=torch.int64)
     else:
-        dev = torch.device(device or "cpu")
-        nlev = torch.empty(1, dtype=torch.int64, device=dev)
-    _broadcast(nlev, src, group)
-    n_levels = int(nlev.item())
+        nlev = torch.empty(1, dtype=torch.int64)
+    dist.broadcast(nlev, src=src, group=hg)
+    n_levels = int(nlev[0])
     if rank != src:
-        hdr_shapes = torch.empty(3 * n_levels + 2, dtype=torch.int64, device=nlev.device)
-    _broadcast(hdr_shapes, src, group)
-    h = hdr_shapes.cpu().tolist()
+        hdr_shapes = torch.empty(3 * n_levels + 2, dtype=torch.int64)
+    dist.broadcast(hdr_shapes, src=src, group=hg)
+    h = hdr_shapes.tolist()
     shapes = [tuple(h[3 * i: 3 * i + 3]) for i in range(n_levels)]
     sub_per_img, code = h[-2], h[-1]
     if rank == src:
-        st, nw, w, (lo, hi) = scatter_streams(bs.states, bs.nwords, bs.words, n_levels,
-                                              bs.n_images, src=src, group=group)
+        st, nw, w, nw_h, (lo, hi) = _scatter(bs.states, bs.nwords, bs.words, n_levels,
+                                             bs.n_images, src, group, None, bs.host_nwords)
     else:
-        st, nw, w, (lo, hi) = scatter_streams(None, None, None, n_levels, 0, src=src,
-                                              group=group, device=nlev.device)
-    from .codec import CONV_NAMES
+        st, nw, w, nw_h, (lo, hi) = _scatter(None, None, None, n_levels, 0, src, group,
+                                             device, None)
     meta = {"n_subpixels": sub_per_img * (hi - lo), "conv": CONV_NAMES[code]}
-    return Bitstream(hi - lo, shapes, st, nw, w, None, meta), (lo, hi)
+    return Bitstream(hi - lo, shapes, st, nw, w, None, meta, nw_h), (lo, hi)
 
 
 def _conv_code(bs):
     from .codec import CONV_CODES
-    return CONV_CODES[bs.meta.get("conv", "f32")]
+    conv = bs.meta.get("conv", "f32")
+    if conv not in CONV_CODES:
+        raise ValueError(f"cannot scatter a bitstream with conv mode {conv!r}")
+    return CONV_CODES[conv]
 
 
 def gather_residual(rbs, dst: int = 0, group=None):
@@ -389,10 +501,10 @@ def gather_residual(rbs, dst: int = 0, group=None):
     single-batch order, and the image-aligned index code runs concatenated in rank order.
     Equal shards required.  Returns the merged bitstream on `dst`, None elsewhere."""
     world = dist.get_world_size(group)
-    agree_conv_mode(rbs.flow, group)
     fl = rbs.flow
-    got = gather_streams(fl.states, fl.nwords, fl.words, dst=dst, group=group)
+    agree_shards(fl, group)
+    got = _gather(fl.states, fl.nwords, fl.words, dst, group, fl.host_nwords)
     idx = gather_padded(rbs.idx_words, dst=dst, group=group)
     if got is None:
         return None
-    return _assemble(rbs, world, *got, idx)
+    return _assemble(rbs, world, *got[:3], idx, got[3])

@@ -479,15 +479,19 @@ class FlowEngine:
         prior -> decode_level(l, ws) fills ws['lat'] level l -> flows backward ->
         unsqueeze.  The image lands in ws['img'] (pixel-major, ld 4)."""
         steps = self.inverse_pm_steps(B, decode_level, cond, priors, slot)
-        for _ in steps:
-            pass
-        return self.workspace(B, slot)
+        while True:
+            try:
+                next(steps)
+            except StopIteration as done:
+                return done.value
 
     def inverse_pm_steps(self, B: int, decode_level, cond=None, priors: bool = True,
                          slot: int = 0):
         """inverse_pm as a generator that yields after each level's decode_level and after
         each coupling block, so that the host can interleave the enqueue of several decode
-        lanes (ImageCodec): all launches go to the stream current at the FIRST step."""
+        lanes (ImageCodec): all launches go to the stream current at the FIRST step.  Its
+        return value (StopIteration.value) is the workspace it decoded into -- the caller must
+        use that one, not look the slot up again (the cache may have evicted the key)."""
         L = lib()
         ws = self.workspace(B, slot)
         s = _lib.stream_ptr(self.device)
@@ -534,6 +538,7 @@ class FlowEngine:
                 dst, ldd, Hh, Ww, Cc = ptr(ws["img"]), 4, self.H, self.W, self.C
             check(L.idf_unsqueeze(s, B, Hh, Ww, Cc, self.scale, ptr(x), Lv.ldx, dst, ldd),
                   "unsqueeze")
+        return ws
 
     def image_nchw(self, ws, B, out=None):
         if out is None:

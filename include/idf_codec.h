@@ -84,9 +84,21 @@ int idf_gather_words(void *stream, int64_t nstreams, const int64_t *d_src_off,
                      const int64_t *d_nwords, const int64_t *d_dst_off, const uint32_t *d_src,
                      uint32_t *d_dst);
 
-/* Host-buffer form of ONE reference call (synchronous; copies in and out).
+/* Host-buffer form of ONE reference call (returns when the outputs are in the host buffers).
  * Exactly `encode(state, n, x_, mean_, scale_)` of rans.pyx:37 / `decode` of
- * rans.pyx:69, with words in push order and mean/scale/out in natural order. */
+ * rans.pyx:69, with words in push order (at most n of them) and mean/scale/out in natural
+ * order.  The _on forms run on the caller's `stream` with the caller's device workspace of
+ * at least idf_rans_host_workspace_bytes(n, nwords) bytes (nwords = 0 for encode): async
+ * copies in, the kernels, async copies out, then a sync of that stream only.  The plain forms
+ * keep the reference's signature and do the same on a per-thread non-blocking stream and a
+ * per-thread workspace that only grows (no allocation per call, no device-wide sync). */
+int64_t idf_rans_host_workspace_bytes(int64_t n, int64_t nwords);
+int idf_rans_encode_on(void *stream, void *d_workspace, int64_t workspace_bytes,
+                       uint64_t *state_io, int64_t n, const float *x, const float *mean,
+                       const float *scale, uint32_t *words, int64_t *nwords, int32_t *status);
+int idf_rans_decode_on(void *stream, void *d_workspace, int64_t workspace_bytes,
+                       uint64_t *state_io, const uint32_t *words, int64_t nwords, int64_t n,
+                       const float *mean, const float *scale, float *out, int32_t *status);
 int idf_rans_encode(uint64_t *state_io, int64_t n, const float *x, const float *mean,
                     const float *scale, uint32_t *words, int64_t *nwords, int32_t *status);
 int idf_rans_decode(uint64_t *state_io, const uint32_t *words, int64_t nwords, int64_t n,
@@ -358,7 +370,8 @@ int idf_dequant_u8(void *stream, int32_t B, int32_t C, int32_t H, int32_t W, con
 /* DLogistic.log_prob (distlib.py:40-55) and IDFlows.log_likelihood's reduction
  * (flows.py:154-169): x, mean, logscale hold n_groups contiguous groups of group_len
  * symbols (one level of one image each).  Writes the per-symbol log-probability to d_logp
- * (may be NULL) and each group's sum, in a fixed order, to d_group_sum (f64; may be NULL).
+ * (may be NULL) and each group's sum, in a fixed order, to d_group_sum (f64; may be NULL:
+ * then the launch is a grid-stride elementwise pass over all n_groups*group_len symbols).
  * Per symbol, in the reference's fp32 order: scale = exp(logscale),
  * x+- = ((x +- 0.5/2^nbits) - mean)/scale, lp/ln = logsigmoid(x+-),
  * logP = lp + log((1 - exp(ln - lp)) + eps). */

@@ -227,6 +227,86 @@ def test_scatter_decode_gather_round_trip(tmp_path, world, n_images):
         assert int(r["wn"]) == n_images and int(r["wsub"]) == n_images * 10
 
 
+def _host_group_worker(rank, world, port, out):
+    """The RCCL configuration's traffic split on CPU: sizes / word-count tables / headers on a
+    separate gloo group, payload on the main group.  Full round trip through
+    gather_bitstream / scatter_bitstream; the host word-count tables ride along."""
+    import sys
+    sys.path.insert(0, PKG)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import idfcodec.dist as D
+    from idfcodec.codec import Bitstream
+    D.SEPARATE_HOST_GROUP = True
+    L, per = 2, 3
+    shapes = [(1, 1, N_SYM)] * L
+    pairs = [(l, b) for l in range(L) for b in range(rank * per, (rank + 1) * per)]
+    st, nw, w = _encode(pairs)
+    local = Bitstream(per, shapes, st, nw, w, None, {"n_subpixels": per * 10, "conv": "f32"},
+                      host_nwords=nw.clone())
+    res = {}
+    for step in range(2):  # the second step re-uses the cached index tensors and host group
+        whole = D.gather_bitstream(local, dst=0)
+        mine, (lo, hi) = D.scatter_bitstream(whole, src=0)
+        assert D.host_group() is not None and len(D._HOST_GROUPS) == 1
+        assert torch.equal(mine.host_nwords, mine.nwords.to(torch.int64))
+        assert torch.equal(mine.states, st) and torch.equal(mine.words, w) and (lo, hi) == (
+            rank * per, (rank + 1) * per)
+        if rank == 0:
+            assert torch.equal(whole.host_nwords, whole.nwords.to(torch.int64))
+            res[f"st{step}"], res[f"w{step}"] = whole.states, whole.words
+    if rank == 0:
+        torch.save(res, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_host_metadata_group_round_trip(tmp_path):
+    out = str(tmp_path / "h.pt")
+    mp.spawn(_host_group_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    r = torch.load(out, weights_only=True)
+    st, nw, w = _encode([(l, b) for l in range(2) for b in range(6)])
+    for step in range(2):
+        assert torch.equal(r[f"st{step}"], st) and torch.equal(r[f"w{step}"], w)
+
+
+def _agree_worker(rank, world, port, case, out):
+    import sys
+    sys.path.insert(0, PKG)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from idfcodec.codec import Bitstream
+    from idfcodec.dist import gather_bitstream
+    per = 3 if (case != "ragged" or rank == 0) else 2
+    st, nw, w = _encode([(l, b) for l in range(2) for b in range(per)])
+    meta = {"n_subpixels": per * 10, "conv": "x3" if (case == "mode" and rank == 1) else "f32"}
+    if case == "scratch" and rank == 1:
+        meta["scratch_offsets"] = torch.zeros(2 * per, dtype=torch.int64)
+    bs = Bitstream(per, [(1, 1, N_SYM)] * 2, st, nw, w, None, meta)
+    try:
+        gather_bitstream(bs, dst=0)
+        msg = "ok"
+    except ValueError as e:
+        msg = str(e)
+    with open(out + f".{rank}", "w") as f:
+        f.write(msg)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case,match", [("ragged", "image counts"), ("scratch", "compacted"),
+                                        ("mode", "conv modes")])
+def test_gather_bitstream_refuses_on_every_rank(tmp_path, case, match):
+    """ADVICE r2 (dist.py:330): unequal shards, an uncompacted stream or mixed conv modes are
+    found by one host all-reduce before any point-to-point traffic, and every rank raises (no
+    rank is left blocked in the exchange)."""
+    out = str(tmp_path / "a")
+    mp.spawn(_agree_worker, args=(2, _free_port(), case, out), nprocs=2, join=True)
+    for r in range(2):
+        with open(out + f".{r}") as f:
+            assert match in f.read()
+
+
 def _bcast_worker(rank, world, port, out):
     import sys
     sys.path.insert(0, PKG)

@@ -281,6 +281,39 @@ def test_log_likelihood_matches_reference(golden, in64):
     want = lpos + torch.log(1 - torch.exp(lneg - lpos) + 1e-8)
     got = model.dist.log_prob(lat[0], me[0], ls[0]).cpu()
     assert torch.allclose(got, want, rtol=1e-4, atol=1e-5)
+    # the elementwise (grid-stride) launch and the grouped launch write the same logp
+    from distlib import dlogistic_log_prob
+    grouped = torch.empty_like(lat[0])
+    dlogistic_log_prob(lat[0], me[0], ls[0], groups=2, logp=grouped)
+    assert torch.equal(got, grouped.cpu())
+
+
+def test_log_prob_broadcasts_and_validates(in64):
+    """DLogistic.log_prob broadcasts like the reference's torch ops (0-dim CPU scalars, a
+    [1,C,H,W] mean) and log_likelihood broadcasts per level; malformed inputs raise instead
+    of reaching the kernel (distlib.py:36)."""
+    from distlib import dlogistic_log_prob
+    model, _ = in64
+    g = torch.Generator().manual_seed(5)
+    x = (torch.randint(0, 256, (2, 3, 8, 8), generator=g).float() / 256).cuda()
+    m = torch.rand(1, 3, 8, 8, generator=g)
+    ls = torch.tensor(-3.0)
+    got = model.dist.log_prob(x, m, ls).cpu()
+    xc, mc = x.cpu(), m.expand(2, 3, 8, 8)
+    sc = torch.exp(ls)
+    lpos = F.logsigmoid((xc + 0.5 / 256 - mc) / sc)
+    lneg = F.logsigmoid((xc - 0.5 / 256 - mc) / sc)
+    want = lpos + torch.log(1 - torch.exp(lneg - lpos) + 1e-8)
+    assert got.shape == (2, 3, 8, 8) and torch.allclose(got, want, rtol=1e-4, atol=1e-5)
+    lp, per_level = model.log_likelihood([x], [m.cuda()], [ls.expand(2, 3, 8, 8).cuda()])
+    assert torch.allclose(per_level[0].cpu().double() * x[0].numel(),
+                          want.double().sum(dim=(1, 2, 3)), rtol=1e-5)
+    with pytest.raises(ValueError):
+        dlogistic_log_prob(x, m.cuda(), ls.cuda())          # unbroadcast parameters
+    with pytest.raises(ValueError):
+        dlogistic_log_prob(x, x, x, logp=torch.empty(5, device="cuda"))
+    with pytest.raises(ValueError):
+        dlogistic_log_prob(x, x, x, logp=torch.empty(x.shape))  # host output
 
 
 def test_dequant_kernel_all_256_values():
@@ -332,6 +365,28 @@ def test_host_c_abi_rans_entries_kat1(golden):
     assert L.idf_rans_encode(ctypes.byref(st), 10, p(x), p(m), p(s), p(w0), ctypes.byref(nw),
                              ctypes.byref(status)) == 0
     assert st.value == int(d["chain/state0"]) and np.array_equal(w0[:nw.value], d["chain/words0"])
+    # the stream forms: the caller's stream and device workspace (no allocation in the call);
+    # an undersized workspace is refused before anything runs
+    side = torch.cuda.Stream()
+    need = L.idf_rans_host_workspace_bytes(n, 1102)
+    assert need >= L.idf_rans_host_workspace_bytes(n, 0) > 0
+    ws = torch.empty(need, dtype=torch.uint8, device="cuda")
+    st = ctypes.c_uint64(1 << 32)
+    words2 = np.zeros(n, np.uint32)
+    assert L.idf_rans_encode_on(ctypes.c_void_p(side.cuda_stream), ctypes.c_void_p(ws.data_ptr()),
+                                need, ctypes.byref(st), n, p(x), p(m), p(s), p(words2),
+                                ctypes.byref(nw), ctypes.byref(status)) == 0
+    assert st.value == 28772813360 and np.array_equal(words2[:nw.value], d["kat1/words"])
+    out2 = np.zeros(n, np.float32)
+    assert L.idf_rans_decode_on(ctypes.c_void_p(side.cuda_stream), ctypes.c_void_p(ws.data_ptr()),
+                                need, ctypes.byref(st), p(w), 1102, n, p(m), p(s), p(out2),
+                                ctypes.byref(status)) == 0
+    assert st.value == 1 << 32 and np.array_equal(out2, x)
+    st = ctypes.c_uint64(1 << 32)
+    assert L.idf_rans_decode_on(ctypes.c_void_p(side.cuda_stream), ctypes.c_void_p(ws.data_ptr()),
+                                need - 1, ctypes.byref(st), p(w), 1102, n, p(m), p(s), p(out2),
+                                ctypes.byref(status)) != 0
+    assert st.value == 1 << 32
 
 
 def test_config3_full_batch_1024(oracle):

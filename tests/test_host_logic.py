@@ -318,8 +318,39 @@ def test_bitstream_conv_flag_round_trips():
         bs = Bitstream(1, [(6, 4, 4), (12, 2, 2)], st, nw, w, meta={"n_subpixels": 48, "conv": mode})
         back = Bitstream.from_bytes(bs.to_bytes())
         assert back.meta["conv"] == mode
-    legacy = Bitstream(1, [(6, 4, 4), (12, 2, 2)], st, nw, w)  # written before the flag
-    assert Bitstream.from_bytes(legacy.to_bytes()).meta["conv"] == "f32"
+    legacy = Bitstream(1, [(6, 4, 4), (12, 2, 2)], st, nw, w)  # no conv in meta: exact f32
+    back = Bitstream.from_bytes(legacy.to_bytes())
+    assert back.meta["conv"] == "f32"
+    assert torch.equal(back.host_nwords, nw) and not back.host_nwords.is_cuda
+
+
+def test_version1_container_without_conv_field():
+    """ADVICE r2 (codec.py:432): version-1 files with flags 0 were written by every engine
+    before the conv field existed.  They read as conv 'unrecorded', which every engine but a
+    split-f16 one accepts (the pre-field behaviour); version-1 files with a conv code and
+    version-2 files keep the exact check; an unrecorded file cannot be re-written as v2."""
+    import struct
+    from idfcodec.codec import VERSION, Bitstream
+    shapes = [(6, 4, 4), (12, 2, 2)]
+    st = torch.zeros(4, dtype=torch.int64)
+    nw = torch.ones(4, dtype=torch.int64)
+    raw = Bitstream(2, shapes, st, nw, torch.zeros(4, dtype=torch.int32),
+                    meta={"conv": "f32"}).to_bytes()
+    assert struct.unpack_from("<H", raw, 4)[0] == VERSION == 2
+    v1 = raw[:4] + struct.pack("<HH", 1, 0) + raw[8:]
+    old = Bitstream.from_bytes(v1)
+    assert old.meta["conv"] == "unrecorded"
+    for fam in ("f32", "halo", "gemm", "unfold", "bf16"):
+        _codec_for(shapes, family=fam, wx3=False).check_bitstream(old)
+    with pytest.raises(ValueError, match="predates the conv field"):
+        _codec_for(shapes, family="x3").check_bitstream(old)
+    with pytest.raises(ValueError, match="re-encode"):
+        old.to_bytes()
+    v1_x3 = raw[:4] + struct.pack("<HH", 1, 1) + raw[8:]
+    assert Bitstream.from_bytes(v1_x3).meta["conv"] == "x3"
+    with pytest.raises(ValueError, match="coded with 'bf16'"):
+        _codec_for(shapes, family="x3").check_bitstream(
+            Bitstream.from_bytes(raw[:4] + struct.pack("<HH", 2, 5) + raw[8:]))
 
 
 def _codec_for(levels, family="x3", wx3=True):
