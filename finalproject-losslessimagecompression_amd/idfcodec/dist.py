@@ -23,6 +23,8 @@ With backend "nccl" every tensor must live on the rank's GPU; the CPU tests use 
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -159,9 +161,9 @@ def shard_streams(states, nwords, words, n_levels: int, n_images: int, lo: int, 
 # ranks: no exchange reads a device value back to size its buffers, and the timed step's
 # stream never drains for one.  Only the payload (final states, words) moves over RCCL.
 _HOST_GROUPS: dict = {}
-# tests set this to build the separate gloo group even when `group` is gloo itself, so the
-# RCCL configuration's two-group traffic runs on CPU
-SEPARATE_HOST_GROUP = False
+# build the separate gloo group even when `group` is gloo itself, so the RCCL configuration's
+# two-group traffic runs under gloo (tests; IDF_DIST_HOST_GROUP=separate for the bench rehearsal)
+SEPARATE_HOST_GROUP = os.environ.get("IDF_DIST_HOST_GROUP") == "separate"
 
 
 def host_group(group=None):

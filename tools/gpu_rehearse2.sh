@@ -5,7 +5,7 @@ set -u -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export PYTHONDONTWRITEBYTECODE=1
-IDF_DIST_BACKEND=gloo IDF_SHARE_GPU=1 timeout -k 10 900 python -u bench.py --gpus 2 --steps 3 --warmup 1 \
+IDF_DIST_BACKEND=gloo IDF_SHARE_GPU=1 IDF_DIST_HOST_GROUP=separate timeout -k 10 900 python -u bench.py --gpus 2 --steps 3 --warmup 1 \
   --no-cpu-baseline > gpurun_out/rh2.log 2>&1; rc=$?
 tail -c 3000 gpurun_out/rh2.log
 exit $rc
