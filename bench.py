@@ -52,6 +52,10 @@ def parse():
     ap.add_argument("--batch", type=int, default=B_PER_GPU)
     ap.add_argument("--cpu-baseline-images", type=int, default=64)
     ap.add_argument("--cpu-baseline-runs", type=int, default=3)
+    ap.add_argument("--cpu-baseline-images-per-proc", type=int, default=16)
+    ap.add_argument("--cpu-baseline-split", default=None,
+                    help="PROCSxTHREADS for the CPU-baseline pool (default: one thread per "
+                         "usable CPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-residual", action="store_true",
                     help="skip the residual configs 3-5 extras")
@@ -176,86 +180,210 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(model_cfg, n_img, runs, chunk=16):
-    """The oracle on the host: torch-fp32 flow (oracle/flow_oracle.py) + C rANS
-    (oracle/rans_oracle.c, OpenMP over streams), encode then decode of n_img images in
-    batches of `chunk` (the CPU's best batch: 64 images at once ran ~3x slower per image
-    than 16 at a time on the MI355X host), the median of `runs` timed runs after one
-    warm-up.  Bounded sample; returns Mpx/s, the threads used, the CPU model and the host's
-    CPU count."""
+def _cpu_oracle(model_cfg):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import statistics
-
-    import numpy as np
     import flow_oracle as FO
-    import rans_oracle as RO
     from idfcodec import synthetic
     model = synthetic.build_model(model_cfg)
     sd = {k: v.detach() for k, v in model.state_dict().items()}
-    o = FO.FlowOracle(model_cfg, sd)
+    return FO.FlowOracle(model_cfg, sd)
+
+
+def _cpu_chunk(o, img):
+    """encode then decode one batch with the oracle: (t_enc, t_dec, exact)."""
+    import numpy as np
+    import flow_oracle as FO
+    import rans_oracle as RO
+    n_img = img.shape[0]
+    t0 = time.perf_counter()
+    x = FO.dequant(img)
+    lat, me, ls = o.forward(x)
+    flat = lambda ts: np.concatenate([t.reshape(-1).numpy() for t in ts])  # noqa: E731
+    L = flat(lat)
+    M = flat(me)
+    S = flat([torch.exp(t) for t in ls])
+    sizes = [t[0].numel() for t in lat]
+    off = [0]
+    for n in sizes:
+        off += [off[-1] + n * (b + 1) for b in range(n_img)]
+    off = np.asarray(off, np.int64)
+    fs, words, nw, st = RO.encode_streams(off, L, M, S)
+    t_enc = time.perf_counter() - t0
+
+    def dec(l, m, s):
+        k0 = l * n_img
+        sl = slice(k0, k0 + n_img)
+        o_l = off[k0:k0 + n_img + 1] - off[k0]
+        m_np = m.reshape(-1).numpy()
+        s_np = torch.exp(s).reshape(-1).numpy()
+        w_off = off[k0:k0 + n_img]
+        fs2, out, st2 = RO.decode_streams(o_l, w_off, nw[sl], words, m_np, s_np, fs[sl])
+        return torch.from_numpy(out).view(m.shape)
+
+    t1 = time.perf_counter()
+    xd, _ = o.decode_levels(n_img, dec)
+    t_dec = time.perf_counter() - t1
+    return t_enc, t_dec, bool(torch.equal(xd, x))
+
+
+def _cpu_run(o, img, chunk):
+    te = td = 0.0
+    ok = True
+    for c0 in range(0, img.shape[0], chunk):
+        a, b, e = _cpu_chunk(o, img[c0:c0 + chunk])
+        te, td, ok = te + a, td + b, ok and e
+    return te, td, ok
+
+
+def _cpu_worker(conn, cpus, threads, n_img, chunk, seed):
+    """One process of the CPU-baseline pool: pinned to `cpus`, `threads` torch/OpenMP threads,
+    its own n_img synthetic images.  Never touches the GPU.  Protocol: sends "ready" after
+    the warm-up, then for every "run" message replies (t_enc, t_dec, exact, cpu_s, wall_s)."""
+    os.environ.update(OMP_NUM_THREADS=str(threads), HIP_VISIBLE_DEVICES="",
+                      CUDA_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="")
+    try:
+        os.sched_setaffinity(0, cpus)
+    except (AttributeError, OSError):
+        pass
+    torch.set_num_threads(threads)
+    from idfcodec import configs, synthetic
+    o = _cpu_oracle(configs.get("imagenet64"))
+    img = synthetic.images(n_img, seed=seed)
+    _cpu_chunk(o, img[:1])  # warm-up (oneDNN primitives, the C coder's library)
+    conn.send("ready")
+    while True:
+        msg = conn.recv()
+        if msg != "run":
+            break
+        c0, w0 = time.process_time(), time.perf_counter()
+        te, td, ok = _cpu_run(o, img, chunk)
+        conn.send((te, td, ok, time.process_time() - c0, time.perf_counter() - w0))
+    conn.close()
+
+
+def _cgroup_cpus():
+    """The cgroup v2 CPU quota in CPUs (cpu.max), or None when unlimited / unreadable."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        return None
+
+
+def usable_cpus():
+    """(affine CPUs, cgroup quota in CPUs or None, CPUs of time the process can use)."""
+    affinity = sorted(os.sched_getaffinity(0))
+    quota = _cgroup_cpus()
+    usable = len(affinity)
+    if quota is not None:
+        usable = max(1, min(usable, int(quota + 1e-6)))
+    return affinity, quota, usable
+
+
+class CpuPool:
+    """The CPU baseline's worker pool, started at the top of main() before anything touches
+    the GPU (the workers are spawned processes: no process is started once HIP is live).
+    It covers every CPU the process may run on: sched_getaffinity, capped by the cgroup's CPU
+    quota when there is one (a GPU box grants 16 CPUs of time over 256 affine CPUs --
+    profiles/r03/host_cpu_probe.txt: 64 busy processes get 16.4 CPUs), split into processes x
+    threads, each process on its own CPUs and its own images.  The timed legs run after the
+    GPU timing (the workers only wait on a pipe meanwhile)."""
+
+    def __init__(self, n_img_per_proc, chunk=16, split=None):
+        import multiprocessing as mp
+        self.affinity, self.quota, usable = usable_cpus()
+        self.usable = usable
+        if split:
+            procs, threads = (int(v) for v in split.lower().split("x"))
+        else:
+            threads = 1  # one thread per process: no OpenMP barriers, best CPU throughput
+            procs = usable
+        self.procs, self.threads = procs, threads
+        self.n_img, self.chunk = n_img_per_proc, min(chunk, n_img_per_proc)
+        ctx = mp.get_context("spawn")
+        self.conns, self.workers = [], []
+        for i in range(procs):
+            cpus = self.affinity[(i * threads) % len(self.affinity):][:threads] or self.affinity
+            a, b = ctx.Pipe()
+            w = ctx.Process(target=_cpu_worker, args=(b, cpus, threads, n_img_per_proc,
+                                                      self.chunk, 100 + i), daemon=True)
+            w.start()
+            self.conns.append(a)
+            self.workers.append(w)
+        self.ready = False
+
+    def wait_ready(self, timeout=900):
+        for c in self.conns:
+            if not c.poll(timeout) or c.recv() != "ready":
+                raise RuntimeError("CPU baseline worker failed to start")
+        self.ready = True
+
+    def run(self):
+        """One timed pass: every worker codes its images; returns (wall, per-worker results)."""
+        t0 = time.perf_counter()
+        for c in self.conns:
+            c.send("run")
+        res = [c.recv() for c in self.conns]
+        return time.perf_counter() - t0, res
+
+    def close(self):
+        for c in self.conns:
+            try:
+                c.send("stop")
+            except OSError:
+                pass
+        for w in self.workers:
+            w.join(timeout=30)
+            if w.is_alive():
+                w.terminate()
+
+
+def cpu_baseline_pool(pool, runs):
+    """The oracle on all of the host's usable CPUs: torch-fp32 flow (oracle/flow_oracle.py) +
+    C rANS (oracle/rans_oracle.c), encode then decode, every pool process on its own images in
+    batches of pool.chunk; the median of `runs` timed passes (after each worker's warm-up).
+    cores = CPUs the pool ran on; effective_cpus = the CPU time it got / wall time."""
+    import statistics
+    if not pool.ready:
+        pool.wait_ready()
+    passes = [pool.run() for _ in range(max(1, runs))]
+    walls = [w for w, _ in passes]
+    med = statistics.median(walls)
+    wall, res = passes[walls.index(sorted(walls)[len(walls) // 2])]
+    px = pool.procs * pool.n_img * PX_PER_IMG
+    exact = all(r[2] for _, rs in passes for r in rs)
+    cpu_s = sum(r[3] for r in res)
+    return {"value": round(px / med / 1e6, 5), "unit": "Mpx/s",
+            "cores": pool.procs * pool.threads, "kind": "port",
+            "split": f"{pool.procs} processes x {pool.threads} threads",
+            "affinity_cpus": len(pool.affinity), "cgroup_cpu_quota": pool.quota,
+            "effective_cpus": round(cpu_s / wall, 2),
+            "cpu_model": _cpu_model(), "runs": len(passes),
+            "runs_mpx_s": [round(px / w / 1e6, 5) for w in walls],
+            "sample": (f"{pool.procs} x {pool.n_img} synthetic 64x64 images (one slice per "
+                       f"process, batches of {pool.chunk}), imagenet64 model, encode+decode "
+                       f"(torch-fp32 flow oracle + C rANS oracle), wall time of the whole "
+                       f"pool, median of {len(passes)} passes; median pass "
+                       f"{wall:.2f}s, round trips exact={exact}")}
+
+
+def cpu_baseline(model_cfg, n_img, runs, chunk=16):
+    """The oracle in THIS process with its torch threads (16 on a GPU box: OMP_NUM_THREADS):
+    the round-2 figure, kept as the single-process comparison next to the pool's.  Median of
+    `runs` timed runs after one warm-up."""
+    import statistics
+    o = _cpu_oracle(model_cfg)
+    from idfcodec import synthetic
     img = synthetic.images(n_img, seed=7)
     threads = torch.get_num_threads()
-    o.forward(FO.dequant(img[:1]))  # warm-up (oneDNN primitive creation)
-
-    def once():
-        te = td = 0.0
-        ok = True
-        for c0 in range(0, n_img, chunk):
-            a, b, e = once_chunk(img[c0:c0 + chunk])
-            te, td, ok = te + a, td + b, ok and e
-        return te, td, ok
-
-    def once_chunk(img):
-        n_img = img.shape[0]
-        t0 = time.perf_counter()
-        x = FO.dequant(img)
-        lat, me, ls = o.forward(x)
-        flat = lambda ts: np.concatenate([t.reshape(-1).numpy() for t in ts])  # noqa: E731
-        L = flat(lat)
-        M = flat(me)
-        S = flat([torch.exp(t) for t in ls])
-        sizes = [t[0].numel() for t in lat]
-        off = [0]
-        for n in sizes:
-            off += [off[-1] + n * (b + 1) for b in range(n_img)]
-        off = np.asarray(off, np.int64)
-        fs, words, nw, st = RO.encode_streams(off, L, M, S)
-        t_enc = time.perf_counter() - t0
-
-        def dec(l, m, s):
-            k0 = l * n_img
-            sl = slice(k0, k0 + n_img)
-            o_l = off[k0:k0 + n_img + 1] - off[k0]
-            m_np = m.reshape(-1).numpy()
-            s_np = torch.exp(s).reshape(-1).numpy()
-            w_off = off[k0:k0 + n_img]
-            fs2, out, st2 = RO.decode_streams(o_l, w_off, nw[sl], words, m_np, s_np, fs[sl])
-            return torch.from_numpy(out).view(m.shape)
-
-        t1 = time.perf_counter()
-        xd, _ = o.decode_levels(n_img, dec)
-        t_dec = time.perf_counter() - t1
-        return t_enc, t_dec, bool(torch.equal(xd, x))
-
-    res = [once() for _ in range(max(1, runs))]
+    _cpu_chunk(o, img[:1])
+    res = [_cpu_run(o, img, chunk) for _ in range(max(1, runs))]
     tot = [a + b for a, b, _ in res]
     med = statistics.median(tot)
-    t_enc, t_dec, _ = res[tot.index(sorted(tot)[len(tot) // 2])]
-    exact = all(e for _, _, e in res)
     px = n_img * PX_PER_IMG
-    try:
-        avail = len(os.sched_getaffinity(0))
-    except AttributeError:
-        avail = os.cpu_count()
-    return {"value": round(px / med / 1e6, 5), "unit": "Mpx/s", "cores": threads,
-            "kind": "port", "cpu_model": _cpu_model(), "host_nproc": os.cpu_count(),
-            "affinity_cpus": avail, "runs": len(res),
+    return {"value": round(px / med / 1e6, 5), "threads": threads,
             "runs_mpx_s": [round(px / t / 1e6, 5) for t in tot],
-            "sample": (f"{n_img} synthetic 64x64 images in batches of {chunk}, imagenet64 model, "
-                       f"encode+decode (torch-fp32 flow oracle, {threads} threads + C rANS "
-                       f"oracle), median of "
-                       f"{len(res)} runs; median run enc {t_enc:.2f}s dec {t_dec:.2f}s, "
-                       f"round trips exact={exact}")}
+            "sample": f"{n_img} images in batches of {chunk}, one process, {threads} threads"}
 
 
 def conv_algorithmic_bytes(eng, B):
@@ -338,6 +466,11 @@ def main():
         return 0
     if world != args.gpus:
         raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE={world}")
+    # the CPU baseline's pool starts here, before anything touches the GPU; its timed passes
+    # run after the GPU timing
+    pool = None
+    if not args.no_cpu_baseline and world == 1:
+        pool = CpuPool(args.cpu_baseline_images_per_proc, split=args.cpu_baseline_split)
     # IDF_DIST_BACKEND=gloo IDF_SHARE_GPU=1: every rank on cuda:0, collectives staged through
     # host memory -- a one-GPU rehearsal of the N-rank path (the real run is RCCL, one GPU each)
     backend = os.environ.get("IDF_DIST_BACKEND", "nccl")
@@ -383,6 +516,8 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    if pool is not None:
+        pool.wait_ready()  # the workers' start-up never overlaps the timed steps
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -451,11 +586,18 @@ def main():
     result = None
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
+        if pool is not None:
             try:
-                cpu = cpu_baseline(cfg, args.cpu_baseline_images, args.cpu_baseline_runs)
+                cpu = cpu_baseline_pool(pool, args.cpu_baseline_runs)
             except Exception as e:  # the baseline is reported, never the product
                 cpu = {"value": None, "error": repr(e)}
+            finally:
+                pool.close()
+            try:
+                cpu["single_process"] = cpu_baseline(cfg, args.cpu_baseline_images,
+                                                     args.cpu_baseline_runs)
+            except Exception as e:
+                cpu["single_process"] = {"value": None, "error": repr(e)}
         result = {
             "metric": "encode+decode Mpixels/s (imagenet64, bit-exact round trip)",
             "value": round(value, 4),
