@@ -449,7 +449,9 @@ def residual_extras(args):
         if r is not None:
             out[name] = {k: r[k] for k in ("value", "encode_mpx_s", "decode_mpx_s", "encode_ms",
                                            "decode_ms", "batch_per_gpu", "image", "bpp",
-                                           "round_trip_exact", "dtype", "n_gpus") if k in r} \
+                                           "round_trip_exact", "dtype", "n_gpus",
+                                           "vq_indices_ms", "vq_reconstruct_ms", "vq_conv",
+                                           "roofline") if k in r} \
                 if "error" not in r else r
     return out
 

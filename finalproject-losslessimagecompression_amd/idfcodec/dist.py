@@ -388,6 +388,9 @@ def merge_residual(parts):
     index code runs concatenated)."""
     fl = [p.flow for p in parts]
     modes = {f.meta.get("conv", "f32") for f in fl}
+    if len({p.vq_conv for p in parts}) != 1:
+        raise ValueError("shards' VQ decoders ran different conv modes: re-encode them with "
+                         "one IDF_VQ_CONV before merging")
     if len(modes) != 1:
         raise ValueError(f"shards coded with different conv modes {sorted(modes)}: re-encode "
                          "them in one mode (ImageCodec engine.set_conv_mode) before merging")
@@ -408,10 +411,10 @@ def _assemble(first, world, st, nw, w, idx, nw_host=None):
         meta["n_subpixels"] = meta["n_subpixels"] * world
     flow = Bitstream(fl.n_images * world, fl.level_shapes, st, nw, w, None, meta, nw_h)
     return ResidualBitstream(flow, idx, first.n_images * world, first.image_shape, first.grid,
-                             first.embed_num, first.source_hw)
+                             first.embed_num, first.source_hw, first.vq_conv)
 
 
-def agree_shards(bs, group=None):
+def agree_shards(bs, group=None, vq_conv=None):
     """Before any point-to-point traffic, every rank checks -- on the host group, with one
     MAX all-reduce -- that all shards ran the same conv arithmetic (a tripped split-f16 range
     guard on one rank re-encodes that shard with exact-f32 convs), hold the same number of
@@ -421,9 +424,14 @@ def agree_shards(bs, group=None):
     from .codec import CONV_CODES
     code = CONV_CODES.get(bs.meta.get("conv", "f32"), -1)
     scratch = int("scratch_offsets" in bs.meta)
-    v = torch.tensor([code, -code, bs.n_images, -bs.n_images, scratch], dtype=torch.int64)
+    vq = {None: 0, "f32": 1, "x3": 2}[vq_conv]
+    v = torch.tensor([code, -code, bs.n_images, -bs.n_images, scratch, vq, -vq],
+                     dtype=torch.int64)
     dist.all_reduce(v, op=dist.ReduceOp.MAX, group=host_group(group))
-    hi, neg_lo, n_hi, neg_n_lo, any_scratch = v.tolist()
+    hi, neg_lo, n_hi, neg_n_lo, any_scratch, vq_hi, neg_vq_lo = v.tolist()
+    if vq_hi != -neg_vq_lo:
+        raise ValueError("shards' VQ decoders ran different conv modes (a tripped split-f16 "
+                         "guard on one rank): re-encode with IDF_VQ_CONV=f32 and gather again")
     if any_scratch:
         raise ValueError("a shard's bitstream is not compacted (encode(compact=False)): "
                          "gather compacted bitstreams only")
@@ -504,7 +512,7 @@ def gather_residual(rbs, dst: int = 0, group=None):
     Equal shards required.  Returns the merged bitstream on `dst`, None elsewhere."""
     world = dist.get_world_size(group)
     fl = rbs.flow
-    agree_shards(fl, group)
+    agree_shards(fl, group, rbs.vq_conv)
     got = _gather(fl.states, fl.nwords, fl.words, dst, group, fl.host_nwords)
     idx = gather_padded(rbs.idx_words, dst=dst, group=group)
     if got is None:

@@ -26,6 +26,9 @@ from .codec import Bitstream, ImageCodec
 
 MAGIC = b"IDFR"
 VERSION = 2         # 2 adds the source (pre-pad) image size; version-1 streams still read
+# header flags bit 0: the VQ decoder's 3x3 convs ran as split-f16 products (vq_conv "x3");
+# 0: exact-f32 Winograd (every stream written before the field existed)
+FLAG_VQ_X3 = 1
 
 
 @dataclass
@@ -37,6 +40,7 @@ class ResidualBitstream:
     grid: tuple                 # (h, w) of the VQ indices per image
     embed_num: int
     source_hw: tuple | None = None   # (H, W) before the dataloader's replication pad
+    vq_conv: str = "f32"        # the VQ decoder's conv arithmetic (idfcodec.vq.VQEngine)
 
     @property
     def source_shape(self) -> tuple:
@@ -58,7 +62,10 @@ class ResidualBitstream:
     def to_bytes(self) -> bytes:
         C, H, W = self.image_shape
         sh, sw = self.source_hw or (H, W)
-        hdr = struct.pack("<4sHHIIIIIIIII", MAGIC, VERSION, 0, self.n_images, C, H, W,
+        if self.vq_conv not in ("x3", "f32"):
+            raise ValueError(f"unknown VQ conv mode {self.vq_conv!r}")
+        flags = FLAG_VQ_X3 if self.vq_conv == "x3" else 0
+        hdr = struct.pack("<4sHHIIIIIIIII", MAGIC, VERSION, flags, self.n_images, C, H, W,
                           self.grid[0], self.grid[1], self.embed_num, sh, sw)
         iw = self.idx_words.detach().cpu().numpy().astype("<i4").tobytes()
         fb = self.flow.to_bytes()
@@ -70,6 +77,8 @@ class ResidualBitstream:
         magic, ver, _f, n, C, H, W, h, w, K = struct.unpack_from(fmt, buf, 0)
         if magic != MAGIC or ver not in (1, VERSION):
             raise ValueError("not an IDF residual bitstream")
+        if _f & ~FLAG_VQ_X3:
+            raise ValueError(f"unknown residual bitstream flags {_f:#x}")
         o = struct.calcsize(fmt)
         src = None
         if ver >= 2:
@@ -82,7 +91,8 @@ class ResidualBitstream:
         flow = Bitstream.from_bytes(buf[o:o + lf], device)
         t = torch.from_numpy(iw)
         return cls(flow, t.to(device) if device else t, n, (C, H, W), (h, w), K,
-                   None if src is None or tuple(src) == (H, W) else tuple(src))
+                   None if src is None or tuple(src) == (H, W) else tuple(src),
+                   "x3" if _f & FLAG_VQ_X3 else "f32")
 
 
 class ResidualCodec:
@@ -151,6 +161,7 @@ class ResidualCodec:
         data = self._dequant(img_u8)
         idx = self.vqvae.indices(data)                       # [B, h, w] int32
         rec = self.vqvae.reconstruct(idx)                    # NCHW on the grid
+        vq_conv = self.vqvae.engine().last_decode_mode       # what the receiver must run
         res = self._pointwise(2, data, rec)                  # data - rec
         res_p, _ = self.patch.forward(res, None)
         codec = self._codec()
@@ -166,7 +177,8 @@ class ResidualCodec:
                                   ptr(words)), "pack idx")
         words = words[:nwd]
         return ResidualBitstream(flow, words, B, (C, H, W), tuple(idx.shape[1:]),
-                                 self.vqvae.embed_num, None if src_hw == (H, W) else src_hw)
+                                 self.vqvae.embed_num, None if src_hw == (H, W) else src_hw,
+                                 vq_conv)
 
     @torch.no_grad()
     def decode(self, rbs: ResidualBitstream, verify: bool = True):
@@ -181,7 +193,7 @@ class ResidualCodec:
         idx = torch.empty(n, dtype=torch.int32, device=dev)
         check(lib().idf_unpack_bits(_lib.stream_ptr(dev), B, h * w, self.bits, ptr(words),
                                     ptr(idx)), "unpack idx")
-        rec = self.vqvae.reconstruct(idx.view(B, h, w))
+        rec = self.vqvae.reconstruct(idx.view(B, h, w), conv=rbs.vq_conv)
         codec = self._codec()
         if self.conditional:
             rec_p, _ = self.patch.forward(rec, None)

@@ -3,8 +3,12 @@
 Every convolution is one `idf_conv_taps_f32` launch over a tap table (csrc/vq_kernels.hip):
 Conv2d(k, s, p) is Hc = Ho, isy = s, taps (ky - p, kx - p); ConvTranspose2d(4, 2, 1) is four
 launches, one per output parity (py, px), each a 2x2-tap conv on the input grid.  The 3x3
-stride-1 convs (ResBlocks: 80-85% of the VQ-VAE's FLOPs) run as Winograd F(2x2, 3x3) instead
-(`idf_conv3x3_wino_res`, csrc/conv3_wino.hip, residual add fused before the activation).  Activations
+stride-1 convs (ResBlocks: 80-85% of the VQ-VAE's FLOPs) run as Winograd F(2x2, 3x3) instead,
+residual add fused before the activation: by default as split-f16 products on f16 MFMA
+(`idf_conv3x3_wx3_res`, conv mode "x3", the flow's own conv arithmetic, 1e-5 of fp32) with the
+range guard -- a pass whose guard trips is recomputed with the exact-f32 Winograd kernel
+(`idf_conv3x3_wino_res`, mode "f32").  The decoder's mode is part of the bitstream
+(ResidualBitstream.vq_conv): the receiver rebuilds the same reconstruction.  Activations
 are pixel-major with channel pitch round_up(C, 4); the 3-channel image is padded to 4 with
 zeros (zero weights).  The batch_norm=True variants (BatchNorm after the activation,
 vqvae.py:31-35) are rejected: no north-star config uses them.
@@ -181,22 +185,41 @@ class DevConv:
     def __init__(self, c: TapConv, device, wino: bool = True):
         self.c = c
         self.w = torch.from_numpy(c.w).to(device)
-        self.wino_u = None
+        self.wino_u = self.wx3_u = None
+        self.wx3_yscale = 1.0
         if wino and is_wino(c):
-            from .packing import wino_weights
-            self.wino_u = torch.from_numpy(
-                wino_weights(c.w.astype(np.float64), c.ldw // 16)).to(device)
+            from .packing import wino_transform64, wino_weights, wino_weights_x3
+            nslab = c.ldw // 16
+            U = wino_transform64(c.w.astype(np.float64), nslab)
+            self.wino_u = torch.from_numpy(wino_weights(c.w.astype(np.float64), nslab, U)).to(device)
+            ux3, self.wx3_yscale = wino_weights_x3(c.w.astype(np.float64), nslab, U)
+            self.wx3_u = torch.from_numpy(ux3.view(np.int16)).to(device)
         self.b = torch.from_numpy(c.bias).to(device)
         self.dy = (ctypes.c_int32 * len(c.dy))(*c.dy)
         self.dx = (ctypes.c_int32 * len(c.dx))(*c.dx)
 
 
+VQ_CONV_MODES = ("x3", "f32")
+
+
 class VQEngine:
-    """Device VQ-VAE: indices and reconstruction of a batch of images."""
+    """Device VQ-VAE: indices and reconstruction of a batch of images.
+
+    conv_mode ("x3" default, IDF_VQ_CONV overrides): the arithmetic of the 3x3 ResBlock convs.
+    encode_pm / decode_pm run it and fall back to "f32" for the whole pass when the split-f16
+    range guard trips; last_decode_mode is the mode the last decode_pm ran (what the encoder
+    records for its receiver)."""
 
     def __init__(self, model, device, wino: bool = True):
+        import os
         self.device = device
         self.wino = wino
+        self.conv_mode = os.environ.get("IDF_VQ_CONV", "x3") if wino else "f32"
+        if self.conv_mode not in VQ_CONV_MODES:
+            raise ValueError(f"IDF_VQ_CONV={self.conv_mode!r}: one of {VQ_CONV_MODES}")
+        self.last_decode_mode = self.conv_mode
+        self.flag = torch.zeros(1, dtype=torch.int32, device=device)
+        self._mode = self.conv_mode  # the mode of the pass being run
         self._ws = None
         self.channel = model.channel
         self.D = model.embed_dim
@@ -212,12 +235,20 @@ class VQEngine:
         return (st, [DevConv(c, self.device, self.wino) for c in st.convs])
 
     # ---------------------------------------------------------------- conv runner
-    def _conv(self, s, dc: DevConv, x, B, H, W, ldx, act, out, ldo, Ho, Wo, res=None, ldr=0):
+    def _conv(self, s, dc: DevConv, x, B, H, W, ldx, act, out, ldo, Ho, Wo, res=None, ldr=0,
+              check_in=1):
         c = dc.c
         if dc.wino_u is not None:
             L = lib()
             wsn = int(L.idf_conv3x3_wino_workspace(B, H, W, c.cin, c.cout))
             ws = self._wino_ws(wsn)
+            if self._mode == "x3":
+                check(L.idf_conv3x3_wx3_res(
+                    s, B, H, W, c.cin, ptr(x), ldx, ptr(dc.wx3_u), c.n_alloc // 16,
+                    dc.wx3_yscale, ptr(dc.b), c.cout, ptr(out), ldo,
+                    ptr(res) if res is not None else None, ldr, act, LEAKY, ptr(self.flag),
+                    check_in, ptr(ws) if wsn else None, wsn), "vq wx3 conv")
+                return
             check(L.idf_conv3x3_wino_res(
                 s, B, H, W, c.cin, ptr(x), ldx, ptr(dc.wino_u), c.n_alloc // 16, ptr(dc.b), c.cout,
                 ptr(out), ldo, ptr(res) if res is not None else None, ldr, act, LEAKY,
@@ -237,6 +268,22 @@ class VQEngine:
         if n and (self._ws is None or self._ws.numel() < n):
             self._ws = torch.empty(n, dtype=torch.float32, device=self.device)
         return self._ws
+
+    def _guarded(self, stages, x, B, H, W, C, mode=None):
+        """_run in `mode` (default conv_mode); an "x3" pass whose range guard trips is run
+        again in "f32".  Returns (outputs..., the mode that produced them)."""
+        mode = mode or self.conv_mode
+        if mode not in VQ_CONV_MODES:
+            raise ValueError(f"unknown VQ conv mode {mode!r}")
+        if mode == "x3":
+            self.flag.zero_()
+        self._mode = mode
+        out = self._run(stages, x, B, H, W, C)
+        if mode == "x3" and bool(self.flag.item()):
+            self._mode = mode = "f32"
+            out = self._run(stages, x, B, H, W, C)
+        self._mode = self.conv_mode
+        return out + (mode,)
 
     def _run(self, stages, x, B, H, W, C):
         """Run conv stages on a pixel-major buffer x [B*H*W][round_up(C,4)]."""
@@ -266,7 +313,9 @@ class VQEngine:
                 t = torch.empty_like(x)
                 self._conv(s, dcs[0], x, B, H, W, ldx, _lib.ACT["ReLU"], t, ldx, H, W)
                 y = torch.empty_like(x)
-                self._conv(s, dcs[1], t, B, H, W, ldx, st.act, y, ldx, H, W, res=x, ldr=ldx)
+                # t is a guarded conv output (|t| < 8192): its transform needs no input check
+                self._conv(s, dcs[1], t, B, H, W, ldx, st.act, y, ldx, H, W, res=x, ldr=ldx,
+                           check_in=0)
                 x = y
         return x, H, W, C
 
@@ -279,7 +328,7 @@ class VQEngine:
         x = torch.zeros(P * 4, dtype=torch.float32, device=self.device)
         check(lib().idf_vq_pointwise(s, P, self.channel, 0, ptr(data_pm), 4, None, 0, ptr(x), 4),
               "vq scale in")
-        z, h, w, C = self._run(self.enc, x, B, H, W, self.channel)
+        z, h, w, C, _ = self._guarded(self.enc, x, B, H, W, self.channel)
         assert C == self.D
         idx = torch.empty(B * h * w, dtype=torch.int32, device=self.device)
         check(lib().idf_vq_argmin(s, B * h * w, self.D, ptr(z), round_up(self.D, 4),
@@ -287,16 +336,18 @@ class VQEngine:
               "vq argmin")
         return idx, (h, w), z
 
-    def decode_pm(self, idx, B, h, w):
+    def decode_pm(self, idx, B, h, w, mode=None):
         """indices -> rec on the 1/256 grid, pixel-major [B*H*W][4] (vqvae.py:149-151,
-        trainer.py:606-607: rec = round8(decoder(embed[idx]) * 0.5 + 0.5))."""
+        trainer.py:606-607: rec = round8(decoder(embed[idx]) * 0.5 + 0.5)).  mode: the conv
+        arithmetic to reproduce (a decoder passes the bitstream's vq_conv); default conv_mode
+        with the guard's fallback.  The mode that ran is left in last_decode_mode."""
         s = _lib.stream_ptr(self.device)
         P = B * h * w
         D4 = round_up(self.D, 4)
         v = torch.zeros(P * D4, dtype=torch.float32, device=self.device)
         check(lib().idf_vq_gather(s, P, self.D, ptr(idx), ptr(self.embed), self.D, ptr(v), D4),
               "vq gather")
-        y, H, W, C = self._run(self.dec, v, B, h, w, self.D)
+        y, H, W, C, self.last_decode_mode = self._guarded(self.dec, v, B, h, w, self.D, mode)
         assert C == self.channel
         rec = torch.zeros(B * H * W * 4, dtype=torch.float32, device=self.device)
         check(lib().idf_vq_pointwise(s, B * H * W, C, 1, ptr(y), 4, None, 0, ptr(rec), 4),
@@ -305,10 +356,10 @@ class VQEngine:
 
     def decoder_raw_pm(self, vq_pm, B, h, w):
         """decoder output (tanh range, pixel-major, pitch 4) for a given latent (tests)."""
-        y, H, W, C = self._run(self.dec, vq_pm, B, h, w, self.D)
+        y, H, W, C, _ = self._guarded(self.dec, vq_pm, B, h, w, self.D)
         return y, (H, W)
 
     def encoder_raw_pm(self, x_pm, B, H, W):
         """encoder output (tanh, pixel-major pitch round_up(D,4)) for a scaled input (tests)."""
-        z, h, w, C = self._run(self.enc, x_pm, B, H, W, self.channel)
+        z, h, w, C, _ = self._guarded(self.enc, x_pm, B, H, W, self.channel)
         return z, (h, w)

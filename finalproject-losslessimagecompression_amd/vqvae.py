@@ -141,11 +141,14 @@ class VQVAE(nn.Module):
         idx, (h, w), _ = self.engine().encode_pm(self._to_pm(data), B, H, W)
         return idx.view(B, h, w)
 
-    def reconstruct(self, idx):
-        """indices [B, h, w] -> rec = round8(decoder(embed[idx]) * 0.5 + 0.5), NCHW."""
+    def reconstruct(self, idx, conv=None):
+        """indices [B, h, w] -> rec = round8(decoder(embed[idx]) * 0.5 + 0.5), NCHW.  conv: the
+        decoder's conv arithmetic ("x3" / "f32", a bitstream's vq_conv); default the engine's
+        mode with the range guard's fallback (engine().last_decode_mode tells which ran)."""
         require_device(idx, "VQ indices")
         B, h, w = idx.shape
-        rec, (H, W) = self.engine().decode_pm(idx.to(torch.int32).contiguous().view(-1), B, h, w)
+        rec, (H, W) = self.engine().decode_pm(idx.to(torch.int32).contiguous().view(-1), B, h, w,
+                                              conv)
         return self._to_nchw(rec, B, self.channel, H, W, 4)
 
     # ------------------------------------------------------------ reference API

@@ -39,9 +39,13 @@ def model_for(name):
     return m.cuda().eval(), z
 
 
+@pytest.mark.parametrize("mode", ["x3", "f32"])
 @pytest.mark.parametrize("name", list(CASES))
-def test_vqvae_engine_matches_reference(name):
+def test_vqvae_engine_matches_reference(name, mode):
+    """Both conv modes of the ResBlock 3x3 convs: split-f16 products (the default) and the
+    exact-f32 Winograd kernel; neither's range guard trips on the reference's data."""
     m, z = model_for(name)
+    m.engine().conv_mode = mode
     data = torch.from_numpy(z["data"]).cuda()
     idx = m.indices(data)
     ok = z["d_margin"].reshape(idx.shape) > 1e-4
@@ -59,6 +63,7 @@ def test_vqvae_engine_matches_reference(name):
     # decoder on the reference's indices
     ridx = torch.from_numpy(z["idx"]).cuda()
     rec = m.reconstruct(ridx).cpu().numpy()
+    assert m.engine().last_decode_mode == mode
     dec = z["dec"]
     t = (dec * 0.5 + 0.5) * 256
     tie = np.abs(t - np.floor(t) - 0.5) < 1e-3
@@ -67,6 +72,31 @@ def test_vqvae_engine_matches_reference(name):
     v = e[ridx.long()].permute(0, 3, 1, 2).contiguous()
     y = m.decode(v).cpu().numpy()
     assert np.abs(y - dec).max() < 1e-5
+
+
+def test_vq_range_guard_falls_back_to_f32():
+    """A decoder input far outside the split-f16 range trips the guard: the pass is re-run in
+    exact f32 and equals a pure-f32 run bit for bit; reconstruct(conv=...) reproduces each
+    mode exactly (what a decoder does with the bitstream's vq_conv)."""
+    m, z = model_for("vq_t2_2down")
+    eng = m.engine()
+    eng.conv_mode = "x3"
+    B, D = 2, m.embed_dim
+    from idfcodec.packing import round_up
+    g = torch.Generator().manual_seed(3)
+    h = w = 4
+    v = torch.zeros(B * h * w, round_up(D, 4))
+    v[:, :D] = torch.randn(B * h * w, D, generator=g)
+    big = (v * 1e5).cuda().reshape(-1).contiguous()
+    y, *_, mode = eng._guarded(eng.dec, big, B, h, w, D)
+    assert mode == "f32"
+    y32, *_, mode32 = eng._guarded(eng.dec, big, B, h, w, D, mode="f32")
+    assert mode32 == "f32" and torch.equal(y, y32)
+    ridx = torch.from_numpy(z["idx"]).cuda()
+    for mode in ("x3", "f32"):
+        a = m.reconstruct(ridx, conv=mode)
+        assert eng.last_decode_mode == mode
+        assert torch.equal(a, m.reconstruct(ridx, conv=mode))
 
 
 @pytest.mark.parametrize("name", list(CASES))

@@ -240,6 +240,13 @@ def test_residual_container_roundtrip_and_source_size():
     assert r1.source_hw is None and torch.equal(r1.idx_words, idx)
     with pytest.raises(ValueError):
         ResidualBitstream.from_bytes(b"IDFX" + raw[4:])
+    # header flags bit 0: the VQ decoder's conv mode (0 = exact f32, every older stream)
+    assert r1.vq_conv == "f32" and struct.unpack_from("<H", raw, 6)[0] == 0
+    x3 = ResidualBitstream(flow, idx, 1, (3, 216, 184), (27, 23), 8192, None, "x3").to_bytes()
+    assert struct.unpack_from("<H", x3, 6)[0] == 1
+    assert ResidualBitstream.from_bytes(x3).vq_conv == "x3"
+    with pytest.raises(ValueError, match="flags"):
+        ResidualBitstream.from_bytes(x3[:6] + struct.pack("<H", 6) + x3[8:])
 
 
 # ------------------------------------------------------------------ coder chaining (F4)

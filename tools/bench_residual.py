@@ -39,6 +39,52 @@ DEFAULT_BATCH = {"resflow-cond-imagenet64": 1024, "resflows_smallpatch_split": 8
                  "resflow-patches-vqvae": 32}
 
 
+PEAK_TFLOPS = {"bf16": 2500.0, "x3": 2500.0, "f32": 157.3}  # MI355X_MICROARCH.md dense peaks
+
+
+def flow_conv_roofline(codec, fl, img):
+    """The flow's DenseLayer 3x3 convs (the residual configs' dominant kernel family) timed
+    live: one encode after the timed steps, side-stream rANS off, HIP events around every
+    conv launch on its own stream (idf_dense_block_f32_timed).  Algorithmic FLOPs per launch
+    = 2*P*9*c*g of the unpadded layer; peak = the dense MFMA peak of the arithmetic the
+    launches ran (bf16 / split-f16 on f16 MFMA / f32 MFMA)."""
+    import ctypes
+    from idfcodec import _lib
+    eng = fl.engine()
+    ic = codec._codec()
+    L = _lib.lib()
+    timer = L.idf_timer_create(65536)
+    for b in eng._blocks:
+        b.timer = timer
+    prev = ic.overlap_encode
+    ic.overlap_encode = False
+    try:
+        codec.encode(img)
+        torch.cuda.synchronize()
+        tot, cnt, fl_ = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+        _lib.check(L.idf_timer_summary(timer, _lib.TAG_CONV3X3, ctypes.byref(tot),
+                                       ctypes.byref(cnt), ctypes.byref(fl_)), "timer")
+    finally:
+        ic.overlap_encode = prev
+        for b in eng._blocks:
+            b.timer = None
+        L.idf_timer_destroy(timer)
+    mode = "bf16" if eng.precision == "bf16" else ("x3" if eng.wino and eng.conv_mode == "x3"
+                                                   else "f32")
+    kern = {"bf16": "conv3_bf16_kernel (bf16 MFMA, f32 accumulate)",
+            "x3": "conv3_wino_kernel<..., true, ...> (Winograd, split-f16 products on f16 MFMA)",
+            "f32": "conv3_wino_kernel (Winograd, f32 MFMA)"}[mode]
+    n = max(cnt.value, 1)
+    achieved = fl_.value / (tot.value * 1e-3) / 1e12 if tot.value > 0 else 0.0
+    peak = PEAK_TFLOPS[mode]
+    return {"kernel": "DenseLayer 3x3 conv, 1x1 folded in: " + kern, "bound": "mfma",
+            "launches": cnt.value, "avg_launch_ms": round(tot.value / n, 5),
+            "conv_ms_per_encode": round(tot.value, 3),
+            "algorithmic_gflop_per_launch": round(fl_.value / n / 1e9, 4),
+            "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "conv_mode": mode}
+
+
 def run(config: str, batch: int | None = None, steps: int = 2, warmup: int = 1,
         precision: str | None = None) -> dict | None:
     """One residual config's encode+decode throughput on this rank's GPU (the process group,
@@ -91,6 +137,7 @@ def run(config: str, batch: int | None = None, steps: int = 2, warmup: int = 1,
         td += t2 - t1
     exact = bool(torch.equal(out, img))
     t_idx, t_rec = vq_time()
+    roof = flow_conv_roofline(codec, fl, img)
     if world > 1:
         t = torch.tensor([te, td, t_idx, t_rec, 0.0 if exact else 1.0], device=dev)
         all_reduce(t, dist.ReduceOp.MAX)
@@ -112,6 +159,7 @@ def run(config: str, batch: int | None = None, steps: int = 2, warmup: int = 1,
             "bpp": round(3 * bs.bpd(), 4), "index_bits_share": round(
                 1 - bs.flow.bits() / bs.bits(), 4),
             "round_trip_exact": exact, "scaling": "weak",
+            "vq_conv": rbs.vq_conv, "roofline": roof,
             "dtype": ("bf16 flow convs (f32 accumulate), f32 heads/VQ-VAE/CDF"
                       if fl.engine().precision == "bf16" else "f32"),
             "data": "synthetic uint8, seeded weights"}
