@@ -514,6 +514,13 @@ class ImageCodec:
             else:
                 main = torch.cuda.current_stream(eng.device)
                 eng.ensure_top_prior(eng.workspace(sz[0], 0), _lib.stream_ptr(eng.device))
+                # every lane's per-level stream offsets are built here, on the main stream,
+                # before `go`: built lazily, lane 0 would create the (size, level) entry on its
+                # own stream and lane 1 -- same size -- read it from another stream, unordered
+                # (level 0 of lane 1 decoded from unwritten offsets: a race seen at 2 x 1024)
+                for n_i in set(sz):
+                    for l in range(eng.nsplit):
+                        self.coder.level_streams(n_i, l)
                 go = torch.cuda.Event()
                 go.record(main)
                 top = eng.nsplit - 1

@@ -18,7 +18,10 @@ production-path parity"):
   * the HIP dequant against the oracle for all 256 values;
   * the C-ABI host entries idf_rans_encode / idf_rans_decode (INTEGRATION.md 2) on KAT1;
   * config 3 at its BASELINE batch (1024 images): exact round trip, sampled streams equal
-    the C oracle.
+    the C oracle;
+  * configs 4 and 5: every DenseBlock of every level teacher-forced in
+    x3 mode (packed 4x4 / 2x2 patches, 27x23 LeakyReLU blocks, cat(z, cond) priors), and
+    full-size images' sampled flow streams equal the C oracle.
 """
 import ctypes
 
@@ -198,6 +201,105 @@ def test_config3_bf16_blocks_teacher_forced(cfg3, lvl):
                                                                         mod.act_name)))
     print(f"config 3 level {lvl}: whole-block distance from the fp32 oracle {worst_fp32:.2e}")
     assert worst_fp32 <= 5e-3  # measured 5.2e-4 .. 8.4e-4 (bf16 operands through 12 layers)
+
+
+@pytest.fixture(scope="module")
+def cfg45():
+    """The flow models of BASELINE configs[3]/[4] as their residual codecs build them."""
+    from idfcodec import synthetic
+    out = {}
+    for name in ("resflows_smallpatch_split", "resflow-patches-vqvae"):
+        codec, fl, vq, size = synthetic.build_residual(name)
+        out[name] = (fl, fl.engine())
+    return out
+
+
+# config 4: two levels (4x4, 2x2 after the squeezes of 8x8 patches); config 5: one level
+# (ExtendDim scale 1 keeps the 27x23 patch)
+CFG45_LEVELS = [("resflows_smallpatch_split", 0), ("resflows_smallpatch_split", 1),
+                ("resflow-patches-vqvae", 0)]
+
+
+@pytest.mark.parametrize("name,lvl", CFG45_LEVELS)
+def test_config45_x3_blocks_teacher_forced(cfg45, name, lvl):
+    """every coupling and prior DenseBlock of configs 4/5 as the engine
+    packed them, in x3 mode, whole block teacher-forced against flow_oracle at 1e-5 and every
+    layer against fp64 on the kernel's own input; re-runs bit-identical and batch-invariant.
+    Config 4 (IDFlows on 8x8 patches): 4x4 / 2x2 levels, the packed-small-image stage, with a
+    ragged batch of patches; config 5 (ConditionalFlows on 27x23 patches, ExtendDim scale 1,
+    LeakyReLU, 32-channel couplings): the priors see cat(z, cond) (flows.py:278-327)."""
+    import flow_oracle as FO
+    from idfcodec.modules import run_device_block
+    fl, eng = cfg45[name]
+    assert len(eng.levels) == {"resflows_smallpatch_split": 2, "resflow-patches-vqvae": 1}[name]
+    Lv = eng.levels[lvl]
+    H, W = Lv.h, Lv.w
+    B = 37 if H * W <= 16 else 3  # a ragged count of packed small patches
+    g = torch.Generator().manual_seed(300 + lvl + 17 * len(name))
+    worst = 0.0
+    for bname, mod, db in _blocks(fl, eng, lvl):
+        assert db.desc.wino and db.desc.wx3, (name, bname, "not on the split-f16 Winograd path")
+        x = _grid((B, mod.i_channel, H, W), g)
+        sd = {k: v.detach().cpu() for k, v in mod.state_dict().items()}
+        eng.clear_range_flag()
+        out, feat = run_device_block(db, x.cuda(), return_feat=True)
+        torch.cuda.synchronize()
+        assert not eng.range_flag_tripped(), (name, bname, "split-f16 range guard tripped")
+        e = scaled_err(out, FO.dense_block(x, sd, "", mod.depth, mod.act_name))
+        worst = max(worst, e)
+        assert e <= TOL, (name, lvl, bname, e)
+        featc = feat.cpu()
+        for i in range(mod.depth):
+            el = scaled_err(_layer_out(featc, db.geom, i),
+                            _layer_ref_fp64(featc, db.geom, sd, i, H, W, mod.act_name))
+            assert el <= TOL, (name, lvl, bname, "layer", i, el)
+        again, _ = run_device_block(db, x.cuda())
+        assert torch.equal(again, out), (bname, "re-run differs")
+        part, _ = run_device_block(db, x[1:3].contiguous().cuda())
+        assert torch.equal(part, out[1:3]), (bname, "images 1-2 alone differ from the batch")
+    print(f"{name} level {lvl} ({H}x{W}): worst whole-block {worst:.2e}")
+
+
+def _sampled_streams_vs_oracle(oracle, fl, rbs, seed, n_pick=24):
+    """A sample of a residual bitstream's flow streams equals the C oracle's encode of the
+    device's own latents / means / scales (first, last, level boundaries, random)."""
+    eng = fl.engine()
+    nimg = rbs.flow.n_images
+    ws = eng.workspace(nimg)
+    lat, mean, scale = (ws[k].cpu().numpy() for k in ("lat", "mean", "scale"))
+    off = fl.codec().coder.sym_off(nimg).cpu().numpy()
+    st = rbs.flow.states.cpu().numpy().view(np.uint64)
+    nw = rbs.flow.nwords.cpu().numpy()
+    words = rbs.flow.words.cpu().numpy().view(np.uint32)
+    woff = np.concatenate([[0], np.cumsum(nw)[:-1]])
+    ns = off.size - 1
+    rng = np.random.default_rng(seed)
+    pick = np.unique(np.concatenate([[0, ns - 1, nimg - 1, min(nimg, ns - 1)],
+                                     rng.integers(0, ns, n_pick)]))
+    for k in pick:
+        a, b = int(off[k]), int(off[k + 1])
+        rs, rw = oracle.encode(1 << 32, lat[a:b], mean[a:b], scale[a:b])
+        assert int(st[k]) == rs, k
+        assert np.array_equal(words[woff[k]:woff[k] + nw[k]], rw), k
+    return len(pick)
+
+
+@pytest.mark.parametrize("name,src,B", [("resflows_smallpatch_split", (256, 256), 2),
+                                        ("resflow-patches-vqvae", (215, 178), 4)])
+def test_config45_full_size_streams_vs_oracle(oracle, name, src, B):
+    """configs 4/5 at full image size (256x256 -> 1024 8x8 patches per
+    image; 215x178 replication-padded to 216x184 -> 64 27x23 patches), the whole residual
+    codec in its production modes: sampled flow streams equal the C oracle on the device's
+    own latents/means/scales, and the round trip is exact."""
+    from idfcodec import synthetic
+    codec, fl, vq, size = synthetic.build_residual(name)
+    x = synthetic.images(B, H=src[0], W=src[1], seed=23).cuda()
+    rbs = codec.encode(x)
+    assert rbs.vq_conv == "x3" and rbs.flow.meta.get("conv") == "x3"
+    n = _sampled_streams_vs_oracle(oracle, fl, rbs, seed=len(name))
+    assert n >= 10
+    out, info = codec.decode(rbs)
+    assert info["ok"] and torch.equal(out, x)
 
 
 def _fill_ws(eng, ws, d, B):
@@ -406,24 +508,6 @@ def test_config3_full_batch_1024(oracle):
     B = 1024
     x = synthetic.images(B, H=size[0], W=size[1], seed=21).cuda()
     rbs = codec.encode(x)
-    eng = fl.engine()
-    nimg = rbs.flow.n_images
-    ws = eng.workspace(nimg)
-    lat = ws["lat"].cpu().numpy()
-    mean = ws["mean"].cpu().numpy()
-    scale = ws["scale"].cpu().numpy()
-    off = fl.codec().coder.sym_off(nimg).cpu().numpy()
-    st = rbs.flow.states.cpu().numpy().view(np.uint64)
-    nw = rbs.flow.nwords.cpu().numpy()
-    words = rbs.flow.words.cpu().numpy().view(np.uint32)
-    woff = np.concatenate([[0], np.cumsum(nw)[:-1]])
-    rng = np.random.default_rng(5)
-    ns = off.size - 1
-    pick = np.unique(np.concatenate([[0, ns - 1, nimg - 1, nimg], rng.integers(0, ns, 24)]))
-    for k in pick:
-        a, b = int(off[k]), int(off[k + 1])
-        rs, rw = oracle.encode(1 << 32, lat[a:b], mean[a:b], scale[a:b])
-        assert int(st[k]) == rs, k
-        assert np.array_equal(words[woff[k]:woff[k] + nw[k]], rw), k
+    _sampled_streams_vs_oracle(oracle, fl, rbs, seed=5)
     out, info = codec.decode(rbs)
     assert info["ok"] and torch.equal(out, x)
