@@ -524,13 +524,17 @@ class ImageCodec:
                 go = torch.cuda.Event()
                 go.record(main)
                 top = eng.nsplit - 1
-                # IDF_LANE_STAGGER: "top" (default) -- lane i+1 starts after lane i's top-level
+                # IDF_LANE_STAGGER: "top" -- lane i+1 starts after lane i's top-level
                 # rANS decode; "levels" -- also every other level's decode waits for lane i's
                 # decode of that level; "none" -- no cross-lane order.  The lanes drift
                 # together after the top level (the GPU ran only rANS kernels for 3.7 ms of a
                 # 31 ms decode), but neither "levels", a high-priority lane 0 nor unequal lanes
                 # (IDF_LANE_SPLIT) shortened the decode (profiles/r02/lanes/order_ab.txt).
-                stagger = os.environ.get("IDF_LANE_STAGGER", "top")
+                # "flows0" (default): as "top", and at the bottom level lane i's couplings start
+                # when lane i-1's are done, so lane i's longest rANS decode runs beside lane
+                # i-1's couplings (+0.5-0.9% bench, decode -0.2..0.3 ms, same-box A/B x5 over
+                # two boxes: profiles/r03/lanes_flows); "flows" orders every level so (-2.7%).
+                stagger = os.environ.get("IDF_LANE_STAGGER", "flows0")
                 # The host enqueues the lanes interleaved -- one step (a level's rANS decode, or
                 # one coupling) of each lane in turn -- so that every lane's launches reach the
                 # GPU early: enqueued lane after lane, the second lane's first kernel waited for
@@ -539,8 +543,10 @@ class ImageCodec:
                 # event recorded) before lane i's waits on it.
                 gens, streams = [], self._lane_streams(nl)
                 done = [dict() for _ in range(nl)]  # done[i][l]: lane i decoded level l
+                flows = stagger.startswith("flows")
+                together = stagger == "none" or stagger == "flows"  # every top decode at once
                 for i, st in enumerate(streams):
-                    st.wait_event(go if (stagger != "none" or i == 0) else first)
+                    st.wait_event(go if (not together or i == 0) else first)
                     if i == 0:
                         first = go
                     if self.lane_marks is not None:  # lane start times (tools/lanes_probe.py)
@@ -566,7 +572,42 @@ class ImageCodec:
                     with torch.cuda.stream(st):
                         next(gens[i])
                     go = staggered
-                live = list(range(nl))
+                live = list(range(nl)) if not flows else []
+                if flows:
+                    # "flows": lane i's couplings of a level start once lane i-1's couplings of
+                    # that level are done, so a lane's prior + rANS decode of the next level
+                    # runs beside the other lane's couplings instead of beside its own rANS
+                    # decode (the lanes otherwise drift into phase and both decode a level's
+                    # streams at once, with the chip idle: profiles/r03/lanes_q).  Host order:
+                    # level by level, lane by lane.  "flows0": only the bottom level (the
+                    # longest rANS chains, the largest couplings) is ordered so; the others
+                    # step round-robin as in "top".
+                    flows_done = [None] * nl
+                    for lv in range(eng.nsplit):
+                        ordered = stagger == "flows" or top - lv == 0
+                        if ordered:
+                            for i, st in enumerate(streams):
+                                with torch.cuda.stream(st):
+                                    if lv:  # the previous level's unsqueeze, this level's decode
+                                        next(gens[i])
+                                    if i:
+                                        st.wait_event(flows_done[i - 1])
+                                    for _ in range(eng.nflows):
+                                        next(gens[i])
+                                    flows_done[i] = torch.cuda.Event()
+                                    flows_done[i].record(st)
+                        else:
+                            for k in range(eng.nflows + (1 if lv else 0)):
+                                for i, st in enumerate(streams):
+                                    with torch.cuda.stream(st):
+                                        next(gens[i])
+                    for i, st in enumerate(streams):
+                        with torch.cuda.stream(st):
+                            try:
+                                next(gens[i])
+                                raise RuntimeError("decode lane did not finish after its levels")
+                            except StopIteration as lane_done:
+                                finish(i, off[i], sz[i], lane_done.value)
                 while live:
                     for i in list(live):
                         with torch.cuda.stream(streams[i]):

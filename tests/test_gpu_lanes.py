@@ -35,7 +35,8 @@ def test_lanes_decode_identical(B):
     import os
     saved = {k: os.environ.get(k) for k in ("IDF_LANE_SPLIT", "IDF_LANE_STAGGER")}
     try:
-        for split, stagger in (("0.375", "levels"), ("0.375", "top"), ("0.625", "none")):
+        for split, stagger in (("0.375", "levels"), ("0.375", "top"), ("0.625", "none"),
+                               ("0.5", "flows"), ("0.625", "flows0")):
             os.environ["IDF_LANE_SPLIT"], os.environ["IDF_LANE_STAGGER"] = split, stagger
             out, info = _decode_all(codec, bs, 2)
             assert info["ok"] and torch.equal(out, img), (split, stagger)
