@@ -543,6 +543,7 @@ class ImageCodec:
                 # event recorded) before lane i's waits on it.
                 gens, streams = [], self._lane_streams(nl)
                 done = [dict() for _ in range(nl)]  # done[i][l]: lane i decoded level l
+                prior_done = [None] * nl  # flows: lane i's bottom-level prior enqueued
                 flows = stagger.startswith("flows")
                 together = stagger == "none" or stagger == "flows"  # every top decode at once
                 for i, st in enumerate(streams):
@@ -556,6 +557,9 @@ class ImageCodec:
                     staggered = torch.cuda.Event()
 
                     def dec(l, ws, i=i, st=st, ev=staggered):
+                        if flows and l == 0 and i + 1 < nl:  # the next lane's bottom prior
+                            prior_done[i] = torch.cuda.Event()
+                            prior_done[i].record(st)
                         if stagger == "levels" and i > 0 and l != top:
                             st.wait_event(done[i - 1][l])
                         self.coder.decode_level(bs, B, l, ws, word_off, out_state, out_status,
@@ -565,8 +569,13 @@ class ImageCodec:
                         elif stagger == "levels":
                             done[i][l] = torch.cuda.Event()
                             done[i][l].record(st)
+                    def pre(l, i=i, st=st):
+                        # flows orders: lane i's bottom prior after lane i-1's, so it runs
+                        # beside lane i-1's bottom rANS decode instead of beside its prior
+                        if flows and l == 0 and i > 0 and top > 0:
+                            st.wait_event(prior_done[i - 1])
                     ci = None if cond is None else cond[off[i]:off[i] + sz[i]].contiguous()
-                    gens.append(eng.inverse_pm_steps(sz[i], dec, cond=ci, slot=i))
+                    gens.append(eng.inverse_pm_steps(sz[i], dec, cond=ci, slot=i, pre_prior=pre))
                     # lane i's first step (its top level's rANS decode) is enqueued before lane
                     # i + 1 waits on the event it records
                     with torch.cuda.stream(st):

@@ -486,12 +486,13 @@ class FlowEngine:
                 return done.value
 
     def inverse_pm_steps(self, B: int, decode_level, cond=None, priors: bool = True,
-                         slot: int = 0):
+                         slot: int = 0, pre_prior=None):
         """inverse_pm as a generator that yields after each level's decode_level and after
         each coupling block, so that the host can interleave the enqueue of several decode
         lanes (ImageCodec): all launches go to the stream current at the FIRST step.  Its
         return value (StopIteration.value) is the workspace it decoded into -- the caller must
-        use that one, not look the slot up again (the cache may have evicted the key)."""
+        use that one, not look the slot up again (the cache may have evicted the key).
+        pre_prior(l), if given, is called just before level l's prior is enqueued."""
         L = lib()
         ws = self.workspace(B, slot)
         s = _lib.stream_ptr(self.device)
@@ -503,6 +504,8 @@ class FlowEngine:
             P = B * Lv.h * Lv.w
             x = self._x(ws, l)
             o = offs[l]
+            if pre_prior is not None:
+                pre_prior(l)
             if priors:
                 mean, logs, scale = (ptr(ws[k]) + o * FLOAT for k in ("mean", "logscale", "scale"))
                 if Lv.prior_x_zero and not self.conditional:
