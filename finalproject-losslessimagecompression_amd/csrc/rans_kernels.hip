@@ -41,6 +41,9 @@
 #ifndef IDF_DECODE_STAMPS
 #define IDF_DECODE_STAMPS 0
 #endif
+#ifndef IDF_DECODE_SETTLE
+#define IDF_DECODE_SETTLE 1
+#endif
 #ifndef IDF_DECODE_FAKE_CDF
 #define IDF_DECODE_FAKE_CDF 0
 #endif
@@ -639,18 +642,28 @@ __global__ void __launch_bounds__(64 * WAVES) rans_decode_kernel(
           asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(outi) : "s"(sv), "s"(t) : "m0");
         }
         wnext = (uint32_t)__builtin_amdgcn_readlane((int)wcur, (P - ipos) & 63);
+        // the record's padding dword stays live to here, so the one-ahead boundary read never
+        // lands in it (a write-after-write on a pending LDS read costs a full LDS round trip)
+        asm volatile("" ::"v"(r0));
       };
+      // Look-ahead LDS reads are issued only after an explicit wait for every earlier LDS read
+      // (landed long ago: they were issued a symbol earlier); the wait-count pass then knows the
+      // loaded registers are ready and adds no lgkmcnt(0) inside the chain that would also
+      // wait for the reads just issued (it merges loop-carried loads conservatively).
+      auto lds_settle = [] { __builtin_amdgcn_s_waitcnt(0xC07F); };  // lgkmcnt(0) only
       // two register sets, so the one-ahead reads need no copies; reads past the window's
       // last symbol land in the spare row and are never used
       i4 a0 = *(lds_i4)(uintptr_t)ra, a1 = *(lds_i4)(uintptr_t)(ra + 16);
       int aab = *(lds_i1)(uintptr_t)ba;
       int t = 0;
       for (; t + 1 < cnt; t += 2) {
+        if (IDF_DECODE_SETTLE) lds_settle();
         const i4 b0 = *(lds_i4)(uintptr_t)(ra + 32), b1 = *(lds_i4)(uintptr_t)(ra + 48);
         const int bab = *(lds_i1)(uintptr_t)(ba + 256);
         symbol(a0, a1, aab, t);
         ra += 64;
         ba += 512;
+        if (IDF_DECODE_SETTLE) lds_settle();
         a0 = *(lds_i4)(uintptr_t)ra;
         a1 = *(lds_i4)(uintptr_t)(ra + 16);
         aab = *(lds_i1)(uintptr_t)ba;

@@ -1,7 +1,11 @@
 // Timing harness for the rANS kernels (built per IDF_DECODE_STAMPS by tools/native/Makefile):
 // 256 streams x N symbols of quantized logistic samples, encoded on the device, then the
 // decode timed and checked for a bit-exact round trip.
+#ifdef RANS_SRC  // same-box A/B against a saved copy of the kernel source (ab/, untracked)
+#include RANS_SRC
+#else
 #include "../../finalproject-losslessimagecompression_amd/csrc/rans_kernels.hip"
+#endif
 
 #include <math.h>
 #include <stdio.h>
