@@ -17,7 +17,8 @@ import torch  # noqa: F401  (must precede the CDLL load, see module doc)
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 REPO = os.path.dirname(PKG)
-LIB_PATH = os.path.join(HERE, "libidfcodec.so")
+# IDF_LIB_PATH: another build of the same library (same-box A/B runs in tools/ only)
+LIB_PATH = os.environ.get("IDF_LIB_PATH") or os.path.join(HERE, "libidfcodec.so")
 HEADER = os.path.join(REPO, "include", "idf_codec.h")
 
 IDF_OK = 0
