@@ -112,6 +112,8 @@ SIGNATURES = {
                                            i64, P, i64, i32, f32, P, i32, P, i64]),
     "idf_conv3x3_wk_supported": (ctypes.c_int, [i32, i32]),
     "idf_conv3x3_wk_workspace": (i64, [i32, i32, i32, i32, i32]),
+    "idf_conv3x3_wq": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, f32, P, P, i32, P,
+                                      i32, P, i64, i32, f32, P, i32]),
     "idf_conv3x3_wk": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, f32, P, P, i32, P,
                                       i32, P, i64, i32, f32, P, i32, P, i64]),
     "idf_conv3x3_wk_res": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, f32, P, i32, P,

@@ -317,6 +317,21 @@ int idf_conv3x3_wx3_res(void *stream, int32_t B, int32_t H, int32_t W, int32_t C
                         float slope, uint32_t *d_flag, int32_t check_input,
                         float *d_workspace, int64_t workspace_floats);
 
+/* "wq": the same split-f16 Winograd conv (same products, U layout, range guard and arguments
+ * as idf_conv3x3_wx3), each wave owning all 16 transform positions of 16 tiles so that the
+ * output transform stays in registers (conv3_wq.hip).  Scope: one K split, N a multiple of 48
+ * after rounding to 16 (3 n-fragments per block), tile widths 32 and 16 (32x32 and 16x16
+ * images and wider); IDF_ERR_UNSUPPORTED otherwise.  idf_conv3x3_wx3 itself runs this kernel
+ * wherever it applies (unless the environment sets IDF_WQ=0), so the engine's encoder and
+ * decoder agree; the outputs differ from wx3's own kernel in the last bits (another fixed
+ * summation order).  Replaces the reference's DenseLayer conv (nnlayer.py:48-51, 1x1 folded
+ * in, nnblock.py:53-56). */
+int idf_conv3x3_wq(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, const float *d_x,
+                   int64_t ld_x, const uint16_t *d_u, int32_t nft, float yscale,
+                   const float *d_b3, const float *d_vtap, int32_t ldv, const float *d_bfull,
+                   int32_t N, float *d_out, int64_t ld_out, int32_t act, float slope,
+                   uint32_t *d_flag, int32_t check_input);
+
 /* "wk": the same split-f16 Winograd convs (same products, same 1e-5 contract, same range
  * guard and arguments as idf_conv3x3_wx3 / _wx3_res) with all three products on K=32 MFMAs
  * (v_mfma_f32_16x16x32_f16, 32-channel slabs, one wave per SIMD; conv3_wk.hip).  d_u: uint16
