@@ -20,11 +20,12 @@
 //  * U goes through LDS once per block and slab (48 KiB, double-buffered): each wave reads the
 //    fragments of the row it is about to multiply, one row ahead of its MFMAs.
 //  * Per 16-channel slab s, four phases (rows a = 0..3 of B^T): phase k issues row k-1's 36
-//    MFMAs beside row k's column combinations + f16 split and row k's U reads; phase 0 (after
-//    the slab barrier) issues the previous slab's row-3 MFMAs beside the new slab's patch reads
-//    and row pass, so the barrier and the LDS read latency sit under queued MFMAs.  Slab s+1's
-//    halo and U (register-staged, coalesced 64-B-per-pixel loads) are written in phase 1 and
-//    slab s+2's loads issued in phase 2; one barrier per slab.
+//    MFMAs beside row k's transform + f16 split and row k's U reads; phase 0 (after the slab
+//    barrier) issues the previous slab's row-3 MFMAs beside the new slab's patch reads, so the
+//    barrier and the LDS read latency sit under queued MFMAs.  Slab s+1's U comes by LDS-DMA
+//    (phase 1); its halo (register-staged, coalesced 64-B-per-pixel loads issued four phases
+//    earlier: one wave per SIMD hides no load latency) is written in phase 3, and slab s+2's
+//    halo loads follow.  One barrier per slab.
 //
 // Scope: split-f16 mode, one K split, 3 n-fragments, tile widths 32 and 16 (imagenet64's
 // 32x32 and 16x16 levels, 60% of the codec's GPU time); everything else stays on wx3.
@@ -42,6 +43,13 @@
 #include "wino_common.h"
 
 #pragma clang fp contract(off)
+
+// timing-only ablations (tools/wq_ablate.sh builds; never set in the library build): bit 0 no U
+// pieces, bit 1 no halo loads/writes, bit 2 no slab barrier, bit 3 no U stage reads, bit 4 no
+// transform / split VALU (hi/lo taken from the patch bits)
+#ifndef IDF_WQ_ABLATE
+#define IDF_WQ_ABLATE 0
+#endif
 
 namespace idf {
 namespace wq {
@@ -159,6 +167,7 @@ __global__ void __launch_bounds__(kThreads) conv3_wq_kernel(Args g) {
   w4 hb[kHaloLoads];
   // slab `slab`'s halo into the staging registers (4 lanes x 16 B = one pixel's 64 B)
   auto load_halo = [&](int slab) {
+    if (IDF_WQ_ABLATE & 2) return;
     const int c0 = slab * 16;
     const bool chan_ok = c0 + hq4 < g.C;
 #pragma unroll
@@ -168,12 +177,14 @@ __global__ void __launch_bounds__(kThreads) conv3_wq_kernel(Args g) {
     }
   };
   auto store_halo = [&](int buf) {
+    if (IDF_WQ_ABLATE & 2) return;
 #pragma unroll
     for (int m = 0; m < kHaloLoads; ++m) *(w4*)(lds + buf * kStage + hdst[m]) = hb[m];
   };
   // slab `slab`'s U fragments -> U stage `buf` by LDS-DMA: each piece is one contiguous 1-KiB
   // fragment (the wave's 12 of the block's 48), no staging registers
   auto issue_u1 = [&](int slab, int buf, int k) {
+    if (IDF_WQ_ABLATE & 1) return;
     const uint32_t ubase = (uint32_t)slab * (uint32_t)g.nft * 1024u + (uint32_t)lane * 16u;
     const int c = wave * kULoads + k, pos = c / kNF, j = c - pos * kNF;
     const uint32_t off = ubase + (uint32_t)((pos * nslab * g.nft + nf0 + j) * 1024);
@@ -187,7 +198,10 @@ __global__ void __launch_bounds__(kThreads) conv3_wq_kernel(Args g) {
   // the slab barrier: the U pieces (issued before the 7 halo loads of the slab after next)
   // have landed, every wave's LDS traffic of the slab is done
   static_assert(kHaloLoads == 7, "barrier vmcnt");
-  auto barrier = [] { asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  auto barrier = [] {
+    if (IDF_WQ_ABLATE & 4) asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
 
   // ---- this lane's patch base: tile 16 * wave + (lane & 15), channel quad lane >> 4
   int pbase;
@@ -221,6 +235,14 @@ __global__ void __launch_bounds__(kThreads) conv3_wq_kernel(Args g) {
   auto vsplit = [&](auto ac, h4 (&hl)[4][2]) {
     constexpr int a = decltype(ac)::value;
     using RA = BT<a>;
+    if (IDF_WQ_ABLATE & 16) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        hl[b][0] = __builtin_bit_cast(h4, __builtin_shufflevector(d[a][b], d[a][b], 0, 1));
+        hl[b][1] = __builtin_bit_cast(h4, __builtin_shufflevector(d[a][b], d[a][b], 2, 3));
+      }
+      return;
+    }
     w4 R[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) R[j] = comb<RA::neg0, RA::neg1>(d[RA::i0][j], d[RA::i1][j]);
@@ -260,7 +282,8 @@ __global__ void __launch_bounds__(kThreads) conv3_wq_kernel(Args g) {
         }
 #pragma unroll
       for (int j = 0; j < kNF; ++j)
-        u[b][j] = *(const w4*)(ust + nbuf * kUStage + ((4 * an + b) * kNF + j) * 256 + lane * 4);
+        if (!(IDF_WQ_ABLATE & 8))
+          u[b][j] = *(const w4*)(ust + nbuf * kUStage + ((4 * an + b) * kNF + j) * 256 + lane * 4);
     }
   };
   // The interleave of one phase (a scheduling region of nk MFMAs): the phase's nw halo writes
@@ -304,29 +327,29 @@ __global__ void __launch_bounds__(kThreads) conv3_wq_kernel(Args g) {
     for (int j = 0; j < kNF; ++j) u[b][j] = *(const w4*)(ust + (b * kNF + j) * 256 + lane * 4);
   for (int s = 0; s < S; ++s) {
     const int buf = s & 1;
-    // phase 1: row 0's MFMAs; row 1's operands; slab s+1's halo -> the other stage
+    // phase 1: row 0's MFMAs; row 1's operands; slab s+1's U pieces -> the other stage
     __builtin_amdgcn_sched_barrier(0);
-    // (the halo writes -- their vmcnt wait -- lead; slab s+1's U pieces follow, one per MFMA)
     vsplit(I1{}, hB);
-    store_halo(buf ^ 1);
     {
       const int us = s + 1 < S ? s + 1 : S - 1;
       row(I0{}, I1{}, hA, u, buf, 0, 4, [&](int k) {
         if (k >= 8 && k < 8 + 2 * kULoads && (k & 1) == 0) issue_u1(us, buf ^ 1, (k - 8) >> 1);
       });
     }
-    sched(C<36>{}, C<2>{}, C<kHaloLoads>{}, C<0>{}, C<0>{});
-    // phase 2: row 1's MFMAs; row 2's operands; slab s+2's halo loads
+    sched(C<36>{}, C<2>{}, C<0>{}, C<0>{}, C<0>{});
+    // phase 2: row 1's MFMAs; row 2's operands
     __builtin_amdgcn_sched_barrier(0);
     vsplit(I2{}, hA);
     row(I1{}, I2{}, hB, u, buf, 0, 4, nohook);
-    load_halo(s + 2 < S ? s + 2 : S - 1);
-    sched(C<36>{}, C<2>{}, C<0>{}, C<kHaloLoads>{}, C<20>{});
-    __builtin_amdgcn_sched_barrier(0);
-    // phase 3: row 2's MFMAs; row 3's operands
-    vsplit(I3{}, hB);
-    row(I2{}, I3{}, hA, u, buf, 0, 4, nohook);
     sched(C<36>{}, C<2>{}, C<0>{}, C<0>{}, C<0>{});
+    __builtin_amdgcn_sched_barrier(0);
+    // phase 3: row 2's MFMAs; row 3's operands; slab s+1's halo (loaded four phases ago) -> the
+    // other stage, then slab s+2's halo loads
+    vsplit(I3{}, hB);
+    store_halo(buf ^ 1);
+    row(I2{}, I3{}, hA, u, buf, 0, 4, nohook);
+    load_halo(s + 2 < S ? s + 2 : S - 1);
+    sched(C<36>{}, C<2>{}, C<kHaloLoads>{}, C<kHaloLoads>{}, C<20>{});
     __builtin_amdgcn_sched_barrier(0);
     barrier();
     // phase 0: row 3's MFMAs beside slab s+1's patch reads and row-0 operands (past the last
