@@ -50,6 +50,11 @@
 #ifndef IDF_WQ_ABLATE
 #define IDF_WQ_ABLATE 0
 #endif
+// halo staging: 1 = LDS-DMA pieces (64 slots of one channel quad each), 0 = coalesced
+// register-staged loads + ds_write (four phases ahead)
+#ifndef IDF_WQ_HALO_DMA
+#define IDF_WQ_HALO_DMA 0
+#endif
 
 namespace idf {
 namespace wq {
@@ -164,10 +169,39 @@ __global__ void __launch_bounds__(kThreads) conv3_wq_kernel(Args g) {
       }
     }
   }
-  w4 hb[kHaloLoads];
+  w4 hb[IDF_WQ_HALO_DMA ? 1 : kHaloLoads];
+  // DMA form: this wave's piece m is f = wave + 4m of the stage's 28: channel quad f / 7, halo
+  // slots [64 (f % 7), +64); xsrc = byte offset of the lane's slot pixel at channel 4q of slab 0
+  uint32_t xsrc[kHaloLoads];
+  if constexpr (IDF_WQ_HALO_DMA) {
+    static_assert(kSlots == 7 * 64 && kHaloLoads == 7, "halo DMA pieces");
+#pragma unroll
+    for (int m = 0; m < kHaloLoads; ++m) {
+      const int f = wave + 4 * m, q = f / 7, slot = 64 * (f - 7 * q) + lane;
+      xsrc[m] = kInvalid;
+      if (slot < NH) {
+        const int img = udiv_s(slot, HH * HWc);
+        const int rem = slot - img * HH * HWc;
+        const int hy = udiv_s(rem, HWc), cs = rem - hy * HWc;
+        const int hx = cs < EHc ? 2 * cs : 2 * (cs - EHc) + 1;
+        const int y = y0 + hy - 1, x = x0 + hx - 1;
+        if (b0 + img < g.B && y >= 0 && y < g.H && x >= 0 && x < g.Wd && hx < g.TW + 2)
+          xsrc[m] = (uint32_t)(((((int64_t)img * g.H + y) * g.Wd + x) * g.ldx + 4 * q) * 4);
+      }
+    }
+  }
+  auto issue_halo1 = [&](int slab, int buf, int m) {
+    if (IDF_WQ_ABLATE & 2) return;
+    const int f = wave + 4 * m, q = f / 7, k = f - 7 * q;
+    const int c0 = slab * 16;
+    const uint32_t off =
+        (xsrc[m] != kInvalid && c0 + 4 * q < g.C) ? xsrc[m] + (uint32_t)c0 * 4u : kInvalid;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_ptr_t)(lds + buf * kStage + (q * kSlots + 64 * k) * 4),
+                                             16, off, 0, 0, 0);
+  };
   // slab `slab`'s halo into the staging registers (4 lanes x 16 B = one pixel's 64 B)
   auto load_halo = [&](int slab) {
-    if (IDF_WQ_ABLATE & 2) return;
+    if (IDF_WQ_ABLATE & 2 || IDF_WQ_HALO_DMA) return;
     const int c0 = slab * 16;
     const bool chan_ok = c0 + hq4 < g.C;
 #pragma unroll
@@ -177,7 +211,7 @@ __global__ void __launch_bounds__(kThreads) conv3_wq_kernel(Args g) {
     }
   };
   auto store_halo = [&](int buf) {
-    if (IDF_WQ_ABLATE & 2) return;
+    if (IDF_WQ_ABLATE & 2 || IDF_WQ_HALO_DMA) return;
 #pragma unroll
     for (int m = 0; m < kHaloLoads; ++m) *(w4*)(lds + buf * kStage + hdst[m]) = hb[m];
   };
@@ -199,8 +233,13 @@ __global__ void __launch_bounds__(kThreads) conv3_wq_kernel(Args g) {
   // have landed, every wave's LDS traffic of the slab is done
   static_assert(kHaloLoads == 7, "barrier vmcnt");
   auto barrier = [] {
-    if (IDF_WQ_ABLATE & 4) asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (IDF_WQ_HALO_DMA) {
+      if (IDF_WQ_ABLATE & 4) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
+      if (IDF_WQ_ABLATE & 4) asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
   };
 
   // ---- this lane's patch base: tile 16 * wave + (lane & 15), channel quad lane >> 4
@@ -311,6 +350,10 @@ __global__ void __launch_bounds__(kThreads) conv3_wq_kernel(Args g) {
   // ---- prologue: slab 0 staged, slab 1's halo loading, slab 0's patch, row-0 operands
   const int S = nslab;
   load_halo(0);
+  if constexpr (IDF_WQ_HALO_DMA) {
+#pragma unroll
+    for (int m = 0; m < kHaloLoads; ++m) issue_halo1(0, 0, m);
+  }
   issue_u(0, 0);
   stage_bias(btab, 16 * kNF, nf0 * 16, g.N, g.b3, g.vtap, g.bfull, g.ldv, tid, kThreads);
   store_halo(0);
@@ -332,9 +375,18 @@ __global__ void __launch_bounds__(kThreads) conv3_wq_kernel(Args g) {
     vsplit(I1{}, hB);
     {
       const int us = s + 1 < S ? s + 1 : S - 1;
-      row(I0{}, I1{}, hA, u, buf, 0, 4, [&](int k) {
-        if (k >= 8 && k < 8 + 2 * kULoads && (k & 1) == 0) issue_u1(us, buf ^ 1, (k - 8) >> 1);
-      });
+      if constexpr (IDF_WQ_HALO_DMA) {
+        // 19 pieces (7 halo, 12 U) spread over the 36 MFMAs
+        row(I0{}, I1{}, hA, u, buf, 0, 4, [&](int k) {
+          if ((k & 1) == 0 && k / 2 < kHaloLoads) issue_halo1(us, buf ^ 1, k / 2);
+          else if ((k & 1) == 0 && k / 2 < kHaloLoads + kULoads) issue_u1(us, buf ^ 1, k / 2 - kHaloLoads);
+          if (k == 35) issue_u1(us, buf ^ 1, kULoads - 1);
+        });
+      } else {
+        row(I0{}, I1{}, hA, u, buf, 0, 4, [&](int k) {
+          if (k >= 8 && k < 8 + 2 * kULoads && (k & 1) == 0) issue_u1(us, buf ^ 1, (k - 8) >> 1);
+        });
+      }
     }
     sched(C<36>{}, C<2>{}, C<0>{}, C<0>{}, C<0>{});
     // phase 2: row 1's MFMAs; row 2's operands
