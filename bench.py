@@ -406,7 +406,8 @@ def conv_algorithmic_bytes(eng, B):
 
 def roofline_pass(codec, eng, timer, img):
     """The dominant kernel timed live: one encode of the batch after the timed steps, with the
-    side-stream rANS encode off (every conv launch has the chip to itself) and HIP events
+    side-stream rANS encode and the encode lanes off (every conv launch has the chip to
+    itself) and HIP events
     around every DenseLayer conv launch of every coupling and prior (idf_dense_block_f32_timed
     brackets each launch on the stream it is issued on).  Returns (achieved TF/s,
     average launch ms, launches, algorithmic FLOPs per launch)."""
@@ -414,14 +415,15 @@ def roofline_pass(codec, eng, timer, img):
     from idfcodec import _lib
     for b in eng._blocks:
         b.timer = timer
-    prev = codec.overlap_encode
+    prev, prev_lanes = codec.overlap_encode, codec.enc_lanes
     codec.overlap_encode = False
+    codec.enc_lanes = 1  # one full-batch launch per conv, nothing beside it
     _lib.lib().idf_timer_reset(timer)
     try:
         codec.encode(img)
         torch.cuda.synchronize()
     finally:
-        codec.overlap_encode = prev
+        codec.overlap_encode, codec.enc_lanes = prev, prev_lanes
         for b in eng._blocks:
             b.timer = None
     tot, cnt, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()

@@ -292,6 +292,27 @@ class _LevelEncoder:
             if e0 is not None:
                 coder.trace.append(("encode", nsym, B, e0, coder._mark()))
 
+    def level_lane(self, l: int, ws, img0: int, n_img: int, wsp):
+        """Level l of images [img0, img0 + n_img) from an encode lane's workspace (laid out
+        for n_img images), encoded on the current (lane) stream into this encoder's stream
+        arrays and word scratch at the images' places in the B-image layout: per stream the
+        same launch arithmetic as level(), so the bitstream is identical."""
+        coder, B = self.coder, self.B
+        eng = coder.engine
+        base, nsym, rel = coder.level_streams(n_img, l)  # lane-local symbols
+        gbase = coder.level_streams(B, l)[0] + img0 * eng.levels[l].n_sym
+        k0 = l * B + img0
+        wbytes = lib().idf_rans_encode_workspace_bytes(nsym)
+        s = _lib.stream_ptr(eng.device)
+        e0 = coder._mark()
+        check(lib().idf_rans_encode_streams(
+            s, n_img, nsym, ptr(rel), ptr(ws["lat"]) + 4 * base, ptr(ws["mean"]) + 4 * base,
+            ptr(ws["scale"]) + 4 * base, ptr(self.init) + 8 * k0, ptr(self.final) + 8 * k0,
+            ptr(self.scratch) + 4 * gbase, ptr(self.nwords) + 8 * k0,
+            ptr(self.status) + 4 * k0, ptr(wsp), wbytes), "rans encode")
+        if e0 is not None:
+            coder.trace.append(("encode", nsym, n_img, e0, coder._mark()))
+
     def join(self):
         """The main stream waits for every side-stream launch issued so far."""
         self.main.wait_stream(self.side)
@@ -337,6 +358,9 @@ class ImageCodec:
         self.engine = engine
         self.coder = StreamCoder(engine)
         self.lanes = int(os.environ.get("IDF_LANES", "2")) if lanes is None else int(lanes)
+        # encode lanes (IDF_ENC_LANES): the flow of a batch as equal sub-batches on the lanes'
+        # streams (_encode_lanes); 1 = the one-pass encode with the side-stream level encode
+        self.enc_lanes = int(os.environ.get("IDF_ENC_LANES", "1"))
         # per-level rANS encode on a side stream, overlapped with the next levels' flow
         self.overlap_encode = os.environ.get("IDF_ENC_OVERLAP", "1") == "1"
         self._streams = []
@@ -348,10 +372,65 @@ class ImageCodec:
         if img_u8.dtype != torch.uint8:
             raise TypeError("ImageCodec.encode expects uint8 images")
         B = img_u8.shape[0]
-        return self._encode_guarded(lambda: self.engine.load_u8(img_u8.contiguous()), B, cond,
-                                    compact)
+        img_u8 = img_u8.contiguous()
+        return self._encode_guarded(lambda: self.engine.load_u8(img_u8), B, cond, compact,
+                                    lanes_img=img_u8)
 
-    def _encode_guarded(self, load, B, cond, compact):
+    def _encode_lanes(self, img_u8, B: int, nl: int, compact: bool) -> Bitstream:
+        """Encode lanes (IDF_ENC_LANES): the batch's flow as nl equal sub-batches on the
+        decode lanes' streams and workspace slots, their launches enqueued interleaved (one
+        coupling of each lane in turn), each lane rANS-encoding its levels on its own stream
+        into the shared B-image stream arrays; one lane's HBM-bound coupling heads and
+        serial rANS chains then run beside the other lane's convs.  The convs are
+        batch-invariant, so the bitstream equals the one-lane encode's bit for bit."""
+        eng = self.engine
+        dev = eng.device
+        sz = [B // nl] * nl
+        off = [sum(sz[:i]) for i in range(nl)]
+        streams = self._lane_streams(nl)
+        enc = self.coder.level_encoder(B)
+        # everything the lanes share is built on the main stream before they fork: the word
+        # scratch, per-lane rANS workspaces, every (size, level) stream-offset table, the top
+        # prior
+        nsym_all = B * eng.n_sym_img
+        if getattr(self, "_enc_scratch", None) is None or self._enc_scratch.numel() < nsym_all:
+            self._enc_scratch = torch.empty(nsym_all, dtype=torch.int32, device=dev)
+        enc.scratch = self._enc_scratch
+        wb = lib().idf_rans_encode_workspace_bytes(sz[0] * max(L.n_sym for L in eng.levels))
+        wsps = getattr(self, "_enc_wsp", [])
+        while len(wsps) < nl:
+            wsps.append(torch.empty(0, dtype=torch.uint8, device=dev))
+        for i in range(nl):
+            if wsps[i].numel() < wb:
+                wsps[i] = torch.empty(wb, dtype=torch.uint8, device=dev)
+        self._enc_wsp = wsps
+        for l in range(len(eng.levels)):
+            self.coder.level_streams(sz[0], l)
+        eng.ensure_top_prior(eng.workspace(sz[0], 0), _lib.stream_ptr(dev))
+        main = torch.cuda.current_stream(dev)
+        go = torch.cuda.Event()
+        go.record(main)
+        gens = []
+        for i, st in enumerate(streams):
+            st.wait_event(go)
+            with torch.cuda.stream(st):
+                eng.load_u8(img_u8[off[i]:off[i] + sz[i]], slot=i)
+                gens.append(eng.forward_pm_steps(
+                    sz[i], slot=i, on_level=lambda l, ws, i=i: enc.level_lane(
+                        l, ws, off[i], sz[i], wsps[i])))
+        live = list(range(nl))
+        while live:
+            for i in list(live):
+                with torch.cuda.stream(streams[i]):
+                    try:
+                        next(gens[i])
+                    except StopIteration:
+                        live.remove(i)
+        for st in streams:
+            main.wait_stream(st)
+        return enc.finish(compact=compact)
+
+    def _encode_guarded(self, load, B, cond, compact, lanes_img=None):
         """Encode in the engine's conv mode; if the split-f16 range guard tripped (a value
         beyond its f16 range), recompute the batch with the exact-f32 convs.  The mode that
         produced the streams is recorded in the bitstream (meta['conv'], container flag)."""
@@ -359,14 +438,26 @@ class ImageCodec:
         mode = eng.conv_family
         if mode == "x3":
             eng.clear_range_flag()
+        nl = 1
+        if lanes_img is not None and cond is None and not eng.conditional:
+            nl = max(1, self.enc_lanes)
+            while nl > 1 and (B % nl or B // nl < self.LANE_MIN):
+                nl -= 1
+            if nl > 1:
+                try:
+                    self._lane_streams(nl)
+                except (OSError, AttributeError, _lib.IdfError):
+                    nl = 1  # no separate HIP streams: one lane (same bitstream)
         enc = None
-        if self.overlap_encode:
+        if self.overlap_encode and nl == 1:
             try:
                 enc = self.coder.level_encoder(B)
             except (OSError, AttributeError, _lib.IdfError):
                 # no separate HIP stream available: the one-pass encode (same bitstream)
                 self.overlap_encode = False
-        if enc is not None:
+        if nl > 1:
+            bs = self._encode_lanes(lanes_img, B, nl, compact)
+        elif enc is not None:
             load()
             try:
                 eng.forward_pm(B, cond=cond, on_level=enc.level)

@@ -417,6 +417,18 @@ class FlowEngine:
     def forward_pm(self, B: int, cond=None, slot: int = 0, on_level=None):
         """Runs flows.py:87-116 from ws['img'] (pixel-major, ld 4) for B images.
         Fills ws lat/mean/logscale/scale.  Returns the workspace."""
+        gen = self.forward_pm_steps(B, cond=cond, slot=slot, on_level=on_level)
+        while True:
+            try:
+                next(gen)
+            except StopIteration as done:
+                return done.value
+
+    def forward_pm_steps(self, B: int, cond=None, slot: int = 0, on_level=None):
+        """forward_pm as a generator that yields after each coupling block and after each
+        level's prior (and on_level), so that the host can interleave the enqueue of several
+        encode lanes (ImageCodec): all launches go to the stream current at the FIRST step.
+        Returns (StopIteration.value) the workspace."""
         L = lib()
         ws = self.workspace(B, slot)
         s = _lib.stream_ptr(self.device)
@@ -439,6 +451,7 @@ class FlowEngine:
                 xo = ptr(x2) + Lv.a * FLOAT
                 blk.run(s, B, Lv.h, Lv.w, ptr(ws["feat"]), self.ld_feat, ptr(ws["tmp"]), self.ld_tmp,
                         head_couple(_lib.EPI_COUPLE_ADD, xo, Lv.ldx))
+                yield l
             x, x2 = self._x(ws, l), self._x(ws, l, 1)
             check(L.idf_permute_couple_in(s, P, Lv.C, ptr(self.ids[l][self.nflows]), ptr(x), Lv.ldx,
                                           ptr(x2), Lv.ldx, 0, 0, None, 0), "permute")
@@ -454,6 +467,7 @@ class FlowEngine:
                 self._prior(ws, B, l, s, mean, logs, scale, ptr(x) + Lv.z * FLOAT, Lv.ldx)
             if on_level is not None:  # level l's lat / mean / scale are final
                 on_level(l, ws)
+            yield l
             src, ld_src, H, W, C = ptr(x) + Lv.z * FLOAT, Lv.ldx, Lv.h, Lv.w, Lv.rest
         return ws
 

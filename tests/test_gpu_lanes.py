@@ -100,3 +100,38 @@ def test_overlapped_level_encode_identical(B):
     assert torch.equal(raw.states, ref_raw[0]) and torch.equal(raw.nwords, ref_raw[1])
     out, info = codec.decode(got)
     assert info["ok"] and torch.equal(out, img)
+
+
+@pytest.mark.parametrize("B,lanes", [(16, 2), (48, 2), (64, 4), (18, 2)])
+def test_encode_lanes_identical(B, lanes):
+    """Encode lanes (IDF_ENC_LANES): the flow as sub-batches on the lanes' streams, each lane
+    rANS-encoding its images' streams into the shared arrays -- the bitstream must equal the
+    one-lane encode's bit for bit (states, word counts, words, status), compact or not, and
+    decode exactly."""
+    from idfcodec import configs, synthetic
+    model = synthetic.build_model(configs.get("imagenet64")).cuda()
+    codec = model.codec()
+    img = synthetic.images(B, seed=70 + B).cuda()
+    codec.enc_lanes = 1
+    ref = codec.encode(img)
+    ref_raw = codec.encode(img, compact=False)
+    codec.enc_lanes = lanes
+    try:
+        got = codec.encode(img)
+        got_raw = codec.encode(img, compact=False)
+    finally:
+        codec.enc_lanes = 1
+    torch.cuda.synchronize()
+    for a, b in ((got, ref), (got_raw, ref_raw)):
+        assert torch.equal(a.states, b.states)
+        assert torch.equal(a.nwords, b.nwords)
+        assert torch.equal(a.status, b.status)
+    assert torch.equal(got.words, ref.words)
+    n = int(ref_raw.nwords.sum())
+    off = ref_raw.meta["scratch_offsets"]
+    for k in range(0, ref_raw.nwords.numel(), max(1, ref_raw.nwords.numel() // 7)):
+        o, m = int(off[k]), int(ref_raw.nwords[k])
+        assert torch.equal(got_raw.words[o:o + m], ref_raw.words[o:o + m]), k
+    assert n > 0
+    out, info = codec.decode(got)
+    assert info["ok"] and torch.equal(out, img)
