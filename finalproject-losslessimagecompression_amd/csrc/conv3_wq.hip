@@ -46,7 +46,8 @@
 
 // timing-only ablations (tools/wq_ablate.sh builds; never set in the library build): bit 0 no U
 // pieces, bit 1 no halo loads/writes, bit 2 no slab barrier, bit 3 no U stage reads, bit 4 no
-// transform / split VALU (hi/lo taken from the patch bits)
+// transform / split VALU (hi/lo taken from the patch bits), bit 5 halo loads waited for but not
+// written to LDS, bit 6 halo writes of registers never loaded (zeros)
 #ifndef IDF_WQ_ABLATE
 #define IDF_WQ_ABLATE 0
 #endif
@@ -54,6 +55,11 @@
 // register-staged loads + ds_write (four phases ahead)
 #ifndef IDF_WQ_HALO_DMA
 #define IDF_WQ_HALO_DMA 0
+#endif
+// L2 prefetch of the halo three slabs ahead (register-staged halo only): one 4-B LDS-DMA per
+// halo pixel into a scratch LDS row, so that the real loads, issued a slab later, hit L2
+#ifndef IDF_WQ_PREFETCH
+#define IDF_WQ_PREFETCH 1
 #endif
 
 namespace idf {
@@ -120,7 +126,7 @@ __device__ __forceinline__ void split(const w4& v, h4& h, h4& l) {
 template <int TWC, bool CHK>
 __global__ void __launch_bounds__(kThreads) conv3_wq_kernel(Args g) {
   constexpr int HWc = halo_pitch(TWC), EHc = HWc / 2;
-  __shared__ __attribute__((aligned(16))) float lds[2 * kStage + 2 * kUStage + 16 * 16 * kNF];
+  __shared__ __attribute__((aligned(16))) float lds[2 * kStage + 2 * kUStage + 16 * 16 * kNF + 4 * 64];
   float* const ust = lds + 2 * kStage;
   float* const btab = ust + 2 * kUStage;  // [16 border classes][48]
 
@@ -170,6 +176,10 @@ __global__ void __launch_bounds__(kThreads) conv3_wq_kernel(Args g) {
     }
   }
   w4 hb[IDF_WQ_HALO_DMA ? 1 : kHaloLoads];
+  if (IDF_WQ_ABLATE & 64) {
+#pragma unroll
+    for (int m = 0; m < (IDF_WQ_HALO_DMA ? 1 : kHaloLoads); ++m) hb[m] = w4{0.f, 0.f, 0.f, 0.f};
+  }
   // DMA form: this wave's piece m is f = wave + 4m of the stage's 28: channel quad f / 7, halo
   // slots [64 (f % 7), +64); xsrc = byte offset of the lane's slot pixel at channel 4q of slab 0
   uint32_t xsrc[kHaloLoads];
@@ -190,6 +200,36 @@ __global__ void __launch_bounds__(kThreads) conv3_wq_kernel(Args g) {
       }
     }
   }
+  // prefetch: this wave's slot blocks wave and wave + 4 (of 7), channel quad 0 of each slot
+  constexpr bool PF = IDF_WQ_PREFETCH && !IDF_WQ_HALO_DMA;
+  uint32_t pfsrc[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int slot = 64 * (wave + 4 * m) + lane;
+    pfsrc[m] = kInvalid;
+    if (PF && wave + 4 * m < 7 && slot < NH) {
+      const int img = udiv_s(slot, HH * HWc);
+      const int rem = slot - img * HH * HWc;
+      const int hy = udiv_s(rem, HWc), cs = rem - hy * HWc;
+      const int hx = cs < EHc ? 2 * cs : 2 * (cs - EHc) + 1;
+      const int y = y0 + hy - 1, x = x0 + hx - 1;
+      if (b0 + img < g.B && y >= 0 && y < g.H && x >= 0 && x < g.Wd && hx < g.TW + 2)
+        pfsrc[m] = (uint32_t)((((int64_t)img * g.H + y) * g.Wd + x) * g.ldx * 4);
+    }
+  }
+  float* const pf_sink = lds + 2 * kStage + 2 * kUStage + 16 * 16 * kNF + 64 * wave;
+  auto prefetch = [&](int slab) {
+    if constexpr (PF) {
+      const int c0 = slab * 16;
+      // every wave issues both pieces (wave 3's second reads nothing): the barrier's vmcnt
+      // counts exactly 7 halo loads + 2 prefetches younger than the U pieces
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const uint32_t off = pfsrc[m] != kInvalid && c0 < g.C ? pfsrc[m] + (uint32_t)c0 * 4u : kInvalid;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_ptr_t)pf_sink, 4, off, 0, 0, 0);
+      }
+    }
+  };
   auto issue_halo1 = [&](int slab, int buf, int m) {
     if (IDF_WQ_ABLATE & 2) return;
     const int f = wave + 4 * m, q = f / 7, k = f - 7 * q;
@@ -201,7 +241,7 @@ __global__ void __launch_bounds__(kThreads) conv3_wq_kernel(Args g) {
   };
   // slab `slab`'s halo into the staging registers (4 lanes x 16 B = one pixel's 64 B)
   auto load_halo = [&](int slab) {
-    if (IDF_WQ_ABLATE & 2 || IDF_WQ_HALO_DMA) return;
+    if (IDF_WQ_ABLATE & (2 | 64) || IDF_WQ_HALO_DMA) return;
     const int c0 = slab * 16;
     const bool chan_ok = c0 + hq4 < g.C;
 #pragma unroll
@@ -212,6 +252,11 @@ __global__ void __launch_bounds__(kThreads) conv3_wq_kernel(Args g) {
   };
   auto store_halo = [&](int buf) {
     if (IDF_WQ_ABLATE & 2 || IDF_WQ_HALO_DMA) return;
+    if (IDF_WQ_ABLATE & 32) {  // the loads and their wait, no LDS writes
+#pragma unroll
+      for (int m = 0; m < kHaloLoads; ++m) asm volatile("" ::"v"(hb[m]));
+      return;
+    }
 #pragma unroll
     for (int m = 0; m < kHaloLoads; ++m) *(w4*)(lds + buf * kStage + hdst[m]) = hb[m];
   };
@@ -236,6 +281,9 @@ __global__ void __launch_bounds__(kThreads) conv3_wq_kernel(Args g) {
     if (IDF_WQ_HALO_DMA) {
       if (IDF_WQ_ABLATE & 4) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    } else if (IDF_WQ_PREFETCH) {  // the halo loads and (younger) prefetches may be in flight
+      if (IDF_WQ_ABLATE & 4) asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     } else {
       if (IDF_WQ_ABLATE & 4) asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -403,6 +451,7 @@ __global__ void __launch_bounds__(kThreads) conv3_wq_kernel(Args g) {
     load_halo(s + 2 < S ? s + 2 : S - 1);
     sched(C<36>{}, C<2>{}, C<kHaloLoads>{}, C<kHaloLoads>{}, C<20>{});
     __builtin_amdgcn_sched_barrier(0);
+    prefetch(s + 3 < S ? s + 3 : S - 1);  // after the halo loads: the barrier lets both fly
     barrier();
     // phase 0: row 3's MFMAs beside slab s+1's patch reads and row-0 operands (past the last
     // slab: the last slab again, unused); its U reloads read slab s+1's stage

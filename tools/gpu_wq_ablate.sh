@@ -6,7 +6,7 @@ O=gpurun_out/wq_ablate
 mkdir -p $O
 export PYTHONDONTWRITEBYTECODE=1
 for r in 1 2; do
-  for n in 0 1 2 4 8 16 31; do
+  for n in 0; do
     echo "== wq_$n"
     IDF_LIB_PATH=tools/wq_lib/wq_$n/libidfcodec.so IDF_WQ=1 KB_ONLY=wx3 KB_LEVELS=0,1 KB_LAYERS=3,11 \
       timeout -k 10 120 python3 -u tools/kbench.py 2>&1 | grep -v amdgpu.ids || exit $?
