@@ -59,7 +59,7 @@
 // L2 prefetch of the halo three slabs ahead (register-staged halo only): one 4-B LDS-DMA per
 // halo pixel into a scratch LDS row, so that the real loads, issued a slab later, hit L2
 #ifndef IDF_WQ_PREFETCH
-#define IDF_WQ_PREFETCH 1
+#define IDF_WQ_PREFETCH 0
 #endif
 
 namespace idf {
