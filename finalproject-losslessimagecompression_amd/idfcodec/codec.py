@@ -361,6 +361,8 @@ class ImageCodec:
         # encode lanes (IDF_ENC_LANES): the flow of a batch as equal sub-batches on the lanes'
         # streams (_encode_lanes); 1 = the one-pass encode with the side-stream level encode
         self.enc_lanes = int(os.environ.get("IDF_ENC_LANES", "1"))
+        self._enc_scratch = None  # encode lanes: the B-image word scratch
+        self._enc_wsp = []        # encode lanes: one rANS encode workspace per lane
         # per-level rANS encode on a side stream, overlapped with the next levels' flow
         self.overlap_encode = os.environ.get("IDF_ENC_OVERLAP", "1") == "1"
         self._streams = []
@@ -393,11 +395,11 @@ class ImageCodec:
         # scratch, per-lane rANS workspaces, every (size, level) stream-offset table, the top
         # prior
         nsym_all = B * eng.n_sym_img
-        if getattr(self, "_enc_scratch", None) is None or self._enc_scratch.numel() < nsym_all:
+        if self._enc_scratch is None or self._enc_scratch.numel() < nsym_all:
             self._enc_scratch = torch.empty(nsym_all, dtype=torch.int32, device=dev)
         enc.scratch = self._enc_scratch
         wb = lib().idf_rans_encode_workspace_bytes(sz[0] * max(L.n_sym for L in eng.levels))
-        wsps = getattr(self, "_enc_wsp", [])
+        wsps = self._enc_wsp
         while len(wsps) < nl:
             wsps.append(torch.empty(0, dtype=torch.uint8, device=dev))
         for i in range(nl):
