@@ -540,6 +540,335 @@ __global__ void __launch_bounds__(kThreads) conv3_wq_kernel(Args g) {
   if (!out_ok && g.flag) atomicOr(g.flag, 1u);
 }
 
+
+// ------------------------------------------------------------------------------------------
+// "wp": the same arithmetic at TWO waves per SIMD.  Block = 8 waves, 64 tiles x 48 outputs;
+// wave w owns tile fragment w & 3 at the eight positions of B^T rows 2 rp, 2 rp + 1 (rp =
+// w >> 2): 96 accumulators, so that the SIMD's other wave hides this one's load and LDS
+// latency (wq's single wave cannot).  Per slab: phase A = row r0's MFMAs beside row r1's
+// transform and U reads (into registers: the stage is rewritten after the barrier), the halo
+// writes of slab s+1, its U pieces and slab s+2's halo loads; the barrier; phase B = row r1's
+// MFMAs beside slab s+1's patch reads and row r0's transform.  Epilogue: the wave pair of a
+// tile fragment exchanges its half-row sums of A^T M through LDS (one barrier) and each
+// finishes two of its lanes' four tiles.
+constexpr int kPThreads = 512;
+constexpr int kPHalo = 4;               // halo loads per wave and slab (28 per stage, 8 waves)
+constexpr int kPU = 16 * kNF / 8;       // U pieces per wave and slab
+
+template <int TWC, bool CHK>
+__global__ void __launch_bounds__(kPThreads) conv3_wp_kernel(Args g) {
+  constexpr int HWc = halo_pitch(TWC), EHc = HWc / 2;
+  __shared__ __attribute__((aligned(16))) float lds[2 * kStage + 2 * kUStage + 16 * 16 * kNF];
+  float* const ust = lds + 2 * kStage;
+  float* const btab = ust + 2 * kUStage;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tf = wave & 3, rp = wave >> 2;
+  int bid = blockIdx.x;
+  const int nt = bid - udiv_s(bid, g.n_tiles) * g.n_tiles;
+  bid = udiv_s(bid, g.n_tiles);
+  const int tx_ = bid - udiv_s(bid, g.tiles_x) * g.tiles_x;
+  bid = udiv_s(bid, g.tiles_x);
+  const int tb = udiv_s(bid, g.tiles_y);
+  const int ty_ = bid - tb * g.tiles_y;
+  const int b0 = tb * g.IMGS, y0 = ty_ * g.TH, x0 = tx_ * g.TW;
+  const int HH = g.TH + 2;
+  const int NH = g.IMGS * HH * HWc;
+  const int TTW = g.TW >> 1, TPI = (g.TH >> 1) * TTW;
+  const int nf0 = nt * kNF;
+  const int S = g.nslab;
+
+  const float* xbase = g.X + (int64_t)b0 * g.H * g.Wd * g.ldx;
+  const int64_t xbytes = ((int64_t)g.B * g.H * g.Wd * g.ldx - (int64_t)b0 * g.H * g.Wd * g.ldx) * 4;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)xbase, 0, (int)(xbytes < (int64_t)kInvalid ? xbytes : (int64_t)kInvalid), 0x00020000);
+  const int64_t ubytes = (int64_t)16 * S * g.nft * 1024;
+  const __amdgpu_buffer_rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.U, 0, (int)(ubytes < (int64_t)kInvalid ? ubytes : (int64_t)kInvalid), 0x00020000);
+  // halo staging: load m of this wave covers slot block f = wave + 8 m (16 slots x 4 quads)
+  const int hq4 = 4 * ((lane >> 3) & 3);
+  uint32_t hsrc[kPHalo];
+  int hdst[kPHalo];
+  {
+    const int sl = (lane & 7) + 8 * (lane >> 5), hq = (lane >> 3) & 3;
+#pragma unroll
+    for (int m = 0; m < kPHalo; ++m) {
+      const int slot = 16 * (wave + 8 * m) + sl;
+      hsrc[m] = kInvalid;
+      hdst[m] = (hq * kSlots + (slot < kSlots ? slot : kSlots - 1)) * 4;
+      if (slot < NH) {
+        const int img = udiv_s(slot, HH * HWc);
+        const int rem = slot - img * HH * HWc;
+        const int hy = udiv_s(rem, HWc), cs = rem - hy * HWc;
+        const int hx = cs < EHc ? 2 * cs : 2 * (cs - EHc) + 1;
+        const int y = y0 + hy - 1, x = x0 + hx - 1;
+        if (b0 + img < g.B && y >= 0 && y < g.H && x >= 0 && x < g.Wd && hx < g.TW + 2)
+          hsrc[m] = (uint32_t)(((((int64_t)img * g.H + y) * g.Wd + x) * g.ldx + hq4) * 4);
+      }
+    }
+  }
+  w4 hb[kPHalo];
+  auto load_halo = [&](int slab) {
+    const int c0 = slab * 16;
+    const bool chan_ok = c0 + hq4 < g.C;
+#pragma unroll
+    for (int m = 0; m < kPHalo; ++m) {
+      const uint32_t off = (hsrc[m] != kInvalid && chan_ok) ? hsrc[m] + (uint32_t)c0 * 4u : kInvalid;
+      hb[m] = __builtin_bit_cast(w4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+    }
+  };
+  auto store_halo = [&](int buf) {
+#pragma unroll
+    for (int m = 0; m < kPHalo; ++m)
+      if (wave + 8 * m < 28) *(w4*)(lds + buf * kStage + hdst[m]) = hb[m];  // wave-uniform
+  };
+  auto issue_u1 = [&](int slab, int buf, int k) {
+    const uint32_t ubase = (uint32_t)slab * (uint32_t)g.nft * 1024u + (uint32_t)lane * 16u;
+    const int c = wave * kPU + k, pos = c / kNF, j = c - pos * kNF;
+    const uint32_t off = ubase + (uint32_t)((pos * S * g.nft + nf0 + j) * 1024);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ur, (lds_ptr_t)(ust + buf * kUStage + c * 256), 16,
+                                             off, 0, 0, 0);
+  };
+  // the slab barrier: every U piece landed (the 4 younger halo loads may fly)
+  auto barrier = [] { asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+
+  int pbase;
+  {
+    const int t = 16 * tf + (lane & 15);
+    int img = udiv_s(t, TPI);
+    const int rem = t - img * TPI;
+    const int ty = udiv_s(rem, TTW), tx = rem - ty * TTW;
+    if (img >= g.IMGS) img = 0;
+    pbase = ((lane >> 4) * kSlots + (img * HH + 2 * ty) * HWc + tx) * 4;
+  }
+  auto cs = [](int j) { return (j & 1) ? EHc + (j >> 1) : (j >> 1); };
+
+  w4 acc[8][kNF];
+#pragma unroll
+  for (int p = 0; p < 8; ++p)
+#pragma unroll
+    for (int j = 0; j < kNF; ++j) acc[p][j] = w4{0.f, 0.f, 0.f, 0.f};
+  float gmax = 0.0f;
+
+  auto run = [&](auto rpc) {
+    constexpr int RP = decltype(rpc)::value;
+    constexpr int R0 = 2 * RP, R1 = 2 * RP + 1;
+    using T0 = BT<R0>;
+    using T1 = BT<R1>;
+    // patch rows: row r0 needs T0::i0, T0::i1; row r1 needs T1::i0, T1::i1 (one of them shared)
+    constexpr int XR = (T1::i0 != T0::i0 && T1::i0 != T0::i1) ? T1::i0 : T1::i1;  // the extra row
+    w4 da[4], db[4], dx[4];  // rows T0::i0, T0::i1, XR of the current slab
+    auto fetch_row = [&](int buf, int i, w4 (&d)[4]) {
+      const float* P = lds + buf * kStage + pbase;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[j] = *(const w4*)(P + (i * HWc + cs(j)) * 4);
+    };
+    auto rowsel = [&](int i) -> const w4* { return i == T0::i0 ? da : (i == T0::i1 ? db : dx); };
+    // row a's four V as f16 pairs
+    auto vsplit = [&](auto tc, h4 (&hl)[4][2]) {
+      using TA = decltype(tc);
+      const w4* p0 = rowsel(TA::i0);
+      const w4* p1 = rowsel(TA::i1);
+      w4 R[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) R[j] = comb<TA::neg0, TA::neg1>(p0[j], p1[j]);
+      w4 v[4];
+      v[0] = comb<BT<0>::neg0, BT<0>::neg1>(R[BT<0>::i0], R[BT<0>::i1]);
+      v[1] = comb<BT<1>::neg0, BT<1>::neg1>(R[BT<1>::i0], R[BT<1>::i1]);
+      v[2] = comb<BT<2>::neg0, BT<2>::neg1>(R[BT<2>::i0], R[BT<2>::i1]);
+      v[3] = comb<BT<3>::neg0, BT<3>::neg1>(R[BT<3>::i0], R[BT<3>::i1]);
+#pragma unroll
+      for (int b = 0; b < 4; ++b) split(v[b], hl[b][0], hl[b][1]);
+      if constexpr (CHK) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          gmax = fmaxf(fmaxf(gmax, fmaxf(fabsf(v[b][0]), fabsf(v[b][1]))),
+                       fmaxf(fabsf(v[b][2]), fabsf(v[b][3])));
+      }
+    };
+    auto mfma_pos = [&](int pl, const h4 (&hl)[2], const w4 (&u)[kNF]) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int j = 0; j < kNF; ++j) {
+          const h8 uu = __builtin_bit_cast(h8, u[j]);
+          const h4 uh = __builtin_shufflevector(uu, uu, 0, 1, 2, 3);
+          const h4 ul = __builtin_shufflevector(uu, uu, 4, 5, 6, 7);
+          const h4 av = p == 0 ? hl[1] : hl[0];
+          const h4 bv = p == 1 ? ul : uh;
+          acc[pl][j] = __builtin_amdgcn_mfma_f32_16x16x16f16(av, bv, acc[pl][j], 0, 0, 0);
+        }
+    };
+    auto read_u1 = [&](int buf, int pos, w4 (&u)[kNF]) {
+#pragma unroll
+      for (int j = 0; j < kNF; ++j)
+        u[j] = *(const w4*)(ust + buf * kUStage + (pos * kNF + j) * 256 + lane * 4);
+    };
+    h4 hA[4][2], hB[4][2];
+    w4 u1[4][kNF];  // row r1's U, read before the slab barrier
+    // prologue
+    load_halo(0);
+#pragma unroll
+    for (int k = 0; k < kPU; ++k) issue_u1(0, 0, k);
+    stage_bias(btab, 16 * kNF, nf0 * 16, g.N, g.b3, g.vtap, g.bfull, g.ldv, tid, kPThreads);
+    store_halo(0);
+    __builtin_amdgcn_sched_barrier(0);
+    load_halo(1 < S ? 1 : S - 1);
+    barrier();
+    fetch_row(0, T0::i0, da);
+    fetch_row(0, T0::i1, db);
+    vsplit(T0{}, hA);
+    for (int s = 0; s < S; ++s) {
+      const int buf = s & 1;
+      // phase A: row r0's MFMAs (U read position by position); row r1's operands; slab s+1's
+      // halo writes and U pieces, slab s+2's halo loads
+      __builtin_amdgcn_sched_barrier(0);
+      fetch_row(buf, XR, dx);
+      vsplit(T1{}, hB);
+      store_halo(buf ^ 1);
+      {
+        const int us = s + 1 < S ? s + 1 : S - 1;
+        w4 u0[4][kNF];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          read_u1(buf, 4 * R0 + b, u0[b]);
+          mfma_pos(b, hA[b], u0[b]);
+          issue_u1(us, buf ^ 1, b);
+          if (b < 2) issue_u1(us, buf ^ 1, 4 + b);
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < 4; ++b) read_u1(buf, 4 * R1 + b, u1[b]);
+#pragma unroll
+      for (int k = 0; k < 36; ++k) {
+        if (k < kPHalo) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (k < 28) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+      }
+      // slab s+2's halo loads strictly after the U pieces: the barrier's vmcnt(4) then waits
+      // for exactly the pieces
+      __builtin_amdgcn_sched_barrier(0);
+      load_halo(s + 2 < S ? s + 2 : S - 1);
+      __builtin_amdgcn_sched_barrier(0);
+      barrier();
+      // phase B: row r1's MFMAs beside slab s+1's patch reads and row r0's operands (past the
+      // last slab: the last slab again, unused)
+      fetch_row(buf ^ 1, T0::i0, da);
+      fetch_row(buf ^ 1, T0::i1, db);
+      vsplit(T0{}, hA);
+#pragma unroll
+      for (int b = 0; b < 4; ++b) mfma_pos(4 + b, hB[b], u1[b]);
+#pragma unroll
+      for (int k = 0; k < 36; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (k < 8) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        if (k >= 6) __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  if (rp == 0) run(C<0>{});
+  else run(C<1>{});
+
+  if constexpr (CHK) {
+    float asum = 0.0f;
+#pragma unroll
+    for (int p = 0; p < 8; ++p)
+#pragma unroll
+      for (int j = 0; j < kNF; ++j) asum += (acc[p][j][0] + acc[p][j][1]) + (acc[p][j][2] + acc[p][j][3]);
+    if ((!(gmax < kGuardIn) || !(asum - asum == 0.0f)) && g.flag) atomicOr(g.flag, 1u);
+  }
+
+  // ---- epilogue.  Half-row sums of A^T M for this wave's rows, per (tile r, n-fragment j,
+  // column b): rp = 0 holds m0, m1 -> P = m0 + m1 (row 0 of A^T M), Q = m1 (row 1); rp = 1
+  // holds m2, m3 -> P = m2, Q = -(m2 + m3).  Row 0 = P0 + P1, row 1 = Q0 + Q1 (a fixed order).
+  // rp = 0 finishes tiles r = 0, 1 of its lanes, rp = 1 tiles r = 2, 3: each writes the other
+  // two tiles' (P, Q) to LDS, reads its partner's for its own two.
+  float* xch = lds;  // [8 waves][2 tiles][3 nf][4 b][2][64 lanes] (98 KB, the stages are free)
+  __syncthreads();   // every wave is past its last stage read
+  auto pq = [&](int r, int j, int b, float& P, float& Q) {
+    const float m0 = acc[b][j][r], m1 = acc[4 + b][j][r];  // this wave's rows 2rp, 2rp+1
+    if (rp == 0) { P = m0 + m1; Q = m1; }
+    else { P = m0; Q = -(m0 + m1); }
+  };
+  const int give0 = rp == 0 ? 2 : 0;  // the tiles this wave hands to its partner
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+    for (int j = 0; j < kNF; ++j)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        float P, Q;
+        pq(give0 + rr, j, b, P, Q);
+        float* dst = xch + ((((wave * 2 + rr) * kNF + j) * 4 + b) * 2) * 64 + lane;
+        dst[0] = P;
+        dst[64] = Q;
+      }
+  __syncthreads();
+  const int partner = wave ^ 4, own0 = rp == 0 ? 0 : 2;
+  const int nn = lane & 15;
+  const int64_t obytes = ((int64_t)g.B * g.H * g.Wd - (int64_t)b0 * g.H * g.Wd) * g.ldo * 4;
+  const __amdgpu_buffer_rsrc_t orr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(g.out + (int64_t)b0 * g.H * g.Wd * g.ldo), 0,
+      (int)(obytes < (int64_t)kInvalid ? obytes : (int64_t)kInvalid), 0x00020000);
+  bool out_ok = true;
+  auto epilogue = [&](auto tanh_c) {
+    constexpr bool TANH = decltype(tanh_c)::value;
+    const WAct act(g.act, g.slope);
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      const int r = own0 + rr;
+      const int t = 16 * tf + 4 * (lane >> 4) + r;
+      const int img = udiv_s(t, TPI);
+      const int rem = t - img * TPI;
+      const int ty = udiv_s(rem, TTW), tx = rem - ty * TTW;
+      uint32_t po[4];
+      int pcl[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int y = y0 + 2 * ty + (e >> 1), x = x0 + 2 * tx + (e & 1);
+        const bool ok = img < g.IMGS && b0 + img < g.B && y < g.H && x < g.Wd;
+        po[e] = ok ? (uint32_t)((img * g.H + y) * g.Wd + x) * (uint32_t)(g.ldo * 4) : kInvalid;
+        pcl[e] = bias_class(y, x, g.H, g.Wd) * (16 * kNF) + nn;
+      }
+#pragma unroll
+      for (int j = 0; j < kNF; ++j) {
+        const int n = (nf0 + j) * 16 + nn;
+        float u0[4], u1v[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          float P, Q;
+          pq(r, j, b, P, Q);
+          const float* src = xch + ((((partner * 2 + rr) * kNF + j) * 4 + b) * 2) * 64 + lane;
+          const float Po = src[0], Qo = src[64];
+          // row sums in a fixed order: the rp = 0 half first
+          u0[b] = rp == 0 ? P + Po : Po + P;
+          u1v[b] = rp == 0 ? Q + Qo : Qo + Q;
+        }
+        float Y[4];
+        Y[0] = (u0[0] + u0[1]) + u0[2];
+        Y[1] = (u0[1] - u0[2]) - u0[3];
+        Y[2] = (u1v[0] + u1v[1]) + u1v[2];
+        Y[3] = (u1v[1] - u1v[2]) - u1v[3];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = Y[e] * g.yscale + btab[pcl[e] + j * 16];
+          v = TANH ? wact(v, g.act, g.slope) : act(v);
+          const bool st = po[e] != kInvalid && n < g.N;
+          out_ok = out_ok && (!st || fabsf(v) < kGuardOut);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), orr,
+                                                st ? po[e] + (uint32_t)n * 4u : kInvalid, 0, 0);
+        }
+      }
+    }
+  };
+  if (g.act == IDF_ACT_TANH) epilogue(std::true_type{});
+  else epilogue(std::false_type{});
+  if (!out_ok && g.flag) atomicOr(g.flag, 1u);
+}
+
 }  // namespace wq
 
 // Launch the wq kernel when the geometry and mode are its scope; IDF_ERR_UNSUPPORTED otherwise
@@ -573,9 +902,20 @@ int wq_launch(void* stream, int32_t B, int32_t H, int32_t W, int32_t C, const fl
   const int64_t blocks = (int64_t)tiles_b * g.tiles_y * g.tiles_x * g.n_tiles;
   if (blocks >= (1 << 20) || nslab >= (1 << 20)) return IDF_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
+  // IDF_WQ_VARIANT=p: the two-waves-per-SIMD form (conv3_wp_kernel)
+  static const bool wp = [] {
+    const char* e = getenv("IDF_WQ_VARIANT");
+    return e && e[0] == 'p';
+  }();
 #define IDF_WQ_LAUNCH(twc, chk)                                                                 \
-  hipLaunchKernelGGL((wq::conv3_wq_kernel<twc, chk>), dim3((unsigned)blocks), dim3(wq::kThreads), \
-                     0, s, g)
+  do {                                                                                          \
+    if (wp)                                                                                     \
+      hipLaunchKernelGGL((wq::conv3_wp_kernel<twc, chk>), dim3((unsigned)blocks),               \
+                         dim3(wq::kPThreads), 0, s, g);                                         \
+    else                                                                                        \
+      hipLaunchKernelGGL((wq::conv3_wq_kernel<twc, chk>), dim3((unsigned)blocks),               \
+                         dim3(wq::kThreads), 0, s, g);                                          \
+  } while (0)
   if (pl.TW == 32) { if (check_input) IDF_WQ_LAUNCH(32, true); else IDF_WQ_LAUNCH(32, false); }
   else { if (check_input) IDF_WQ_LAUNCH(16, true); else IDF_WQ_LAUNCH(16, false); }
 #undef IDF_WQ_LAUNCH
