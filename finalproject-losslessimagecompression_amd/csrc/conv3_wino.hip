@@ -86,6 +86,10 @@
 #ifndef IDF_X3_FAKE32
 #define IDF_X3_FAKE32 0
 #endif
+// XCD-aware block order (wino_common.h wino_xcd_remap): 1 = on
+#ifndef IDF_WINO_XCD
+#define IDF_WINO_XCD 1
+#endif
 // timing-only in-kernel s_memtime stamps (tools/native/wino_ablate wino_stamps builds)
 #ifndef IDF_WINO_STAMPS
 #define IDF_WINO_STAMPS 0
@@ -456,7 +460,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   const uint64_t st_k0 = IDF_WINO_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  int bid = blockIdx.x;
+  int bid = IDF_WINO_XCD ? wino_xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
   const int ks = bid - udiv_s(bid, g.ksplit) * g.ksplit;
   bid = udiv_s(bid, g.ksplit);
   const int nt = bid - udiv_s(bid, g.n_tiles) * g.n_tiles;
