@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "idf_codec_internal.h"
 
@@ -82,11 +83,23 @@ struct WinoPlan {
 // tiled as the next even size: the extra row/column of 2x2 tiles reads zero padding
 // (out-of-image halo) and its outputs are never stored, so every stored pixel sees the
 // same 3x3 neighbourhood as in the direct conv.
+// Output tile width of images exactly 32 wide (imagenet64's 32x32 level): 16 (16x16 blocks, 4 per
+// image; bench +0.7% same-box over 32x8 strips, profiles/r03/session2/tw_ab.txt) unless
+// IDF_WINO_TW32=32.  The tiling never changes a tile's arithmetic: the outputs are the same
+// bits either way.
+static inline int wino_tw_32() {
+  static const int tw = [] {
+    const char* e = getenv("IDF_WINO_TW32");
+    return e && atoi(e) == 32 ? 32 : 16;
+  }();
+  return tw;
+}
+
 static inline WinoPlan wino_plan(int H, int W, int nslab, int N) {
   WinoPlan pl = {0, 1, 0, 0, 1, 0};
   if (H < 1 || W < 1) return pl;
   const int He = (H + 1) & ~1, We = (W + 1) & ~1;
-  pl.TW = We < 32 ? We : 32;
+  pl.TW = We < 32 ? We : (We == 32 ? wino_tw_32() : 32);
   pl.TH = 256 / pl.TW;  // 64 wino tiles = 256 output pixels
   if (pl.TH > He) pl.TH = He;
   if (pl.TH & 1) pl.TH -= 1;
