@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(kBThreads) conv3_bf16_kernel(Bf16Args g) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  int bid = blockIdx.x;
+  int bid = xcd_contiguous(blockIdx.x, gridDim.x);  // neighbouring tiles on one XCD
   const int ks = bid % g.ksplit;
   bid /= g.ksplit;
   const int tx_ = bid % g.tiles_x;

@@ -15,6 +15,20 @@ static inline int idf_last_error() {
 
 namespace idf {
 
+// XCD-aware block order: the dispatcher deals blocks round-robin over the 8 XCDs (block b on
+// XCD b % 8); this bijection gives XCD x a contiguous range of tile indices instead, so tiles
+// that share input rows (conv halos) run on one XCD and share its L2.  Which block computes a
+// tile changes, never the tile's arithmetic.
+__device__ __forceinline__ int xcd_contiguous(int bid, int nwg) {
+#ifdef IDF_XCD_OFF  // timing-only A/B builds (tools/gpu_xcd_res_ab.sh): the dispatcher's order
+  return bid;
+#endif
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = bid % 8, idx = bid / 8;
+  const int start = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return start + idx;
+}
+
 // Border class of an output pixel for the folded 1x1 bias: bit 0 y == 0, bit 1 y == H-1,
 // bit 2 x == 0, bit 3 x == W-1 (class 0 = interior).
 __device__ __forceinline__ int bias_class(int y, int x, int H, int W) {

@@ -76,7 +76,8 @@ __global__ void __launch_bounds__(256) conv_taps_kernel(ConvTapsArgs g) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-  const int mt = blockIdx.x / g.n_tiles, nt = blockIdx.x % g.n_tiles;
+  const int bid = xcd_contiguous(blockIdx.x, gridDim.x);  // neighbouring row tiles on one XCD
+  const int mt = bid / g.n_tiles, nt = bid % g.n_tiles;
   const int64_t m0 = (int64_t)mt * BM;
   const int n0 = nt * BN;
   const int64_t hwc = (int64_t)g.Hc * g.Wc;

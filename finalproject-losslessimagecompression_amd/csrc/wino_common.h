@@ -48,17 +48,9 @@ __device__ __forceinline__ int udiv_s(int a, int b) {
   return q + (r >= b) - (r < 0);
 }
 
-// XCD-aware block order: the dispatcher deals blocks round-robin over the 8 XCDs (block b on
-// XCD b % 8); this bijection gives XCD x a contiguous range of tile indices instead, so the
-// neighbouring tiles of an image -- which share halo rows -- run on one XCD, beside each other,
-// and read the shared rows through that XCD's L2.  Which block computes a tile changes, not
-// the tile's arithmetic: outputs are bit-identical.
-__device__ __forceinline__ int wino_xcd_remap(int bid, int nwg) {
-  const int q = nwg / 8, r = nwg % 8;
-  const int xcd = bid % 8, idx = bid / 8;
-  const int start = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-  return start + idx;
-}
+// XCD-aware block order of the Winograd kernels (idf_codec_internal.h xcd_contiguous): the
+// neighbouring tiles of an image run on one XCD and read their shared halo rows through its L2.
+__device__ __forceinline__ int wino_xcd_remap(int bid, int nwg) { return xcd_contiguous(bid, nwg); }
 
 // B^T of F(2,3): row a combines d[I0(a)] (sign S0(a)) and d[I1(a)] (sign S1(a)).
 template <int a> struct BT {
