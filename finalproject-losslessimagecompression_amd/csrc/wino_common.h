@@ -87,11 +87,20 @@ static inline int wino_tw_32() {
   return tw;
 }
 
+// Output tile width of images wider than 32 (the VQ-VAE's convs): 32 unless IDF_WINO_TWW=16.
+static inline int wino_tw_wide() {
+  static const int tw = [] {
+    const char* e = getenv("IDF_WINO_TWW");
+    return e && atoi(e) == 16 ? 16 : 32;
+  }();
+  return tw;
+}
+
 static inline WinoPlan wino_plan(int H, int W, int nslab, int N) {
   WinoPlan pl = {0, 1, 0, 0, 1, 0};
   if (H < 1 || W < 1) return pl;
   const int He = (H + 1) & ~1, We = (W + 1) & ~1;
-  pl.TW = We < 32 ? We : (We == 32 ? wino_tw_32() : 32);
+  pl.TW = We < 32 ? We : (We == 32 ? wino_tw_32() : wino_tw_wide());
   pl.TH = 256 / pl.TW;  // 64 wino tiles = 256 output pixels
   if (pl.TH > He) pl.TH = He;
   if (pl.TH & 1) pl.TH -= 1;
