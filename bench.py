@@ -79,27 +79,52 @@ def launch(args) -> int:
     return subprocess.call(cmd)
 
 
-def pmc_traffic(kernel: str, n_last: int, extra: str = "conv3_wino_reduce_kernel"):
-    """HBM bytes per launch of `kernel` from the newest committed PMC passes
+# the sources whose compiled kernels a committed PMC traffic capture describes
+CONV_SOURCES = ("conv3_dx3.hip", "conv3_wino.hip", "wino_common.h", "idf_codec_internal.h")
+
+
+def conv_source_hash() -> str:
+    """sha256 over the conv kernels' sources (CONV_SOURCES, in order): tools/pmc_bench.sh stores
+    it with a capture (source_hash.txt) and pmc_traffic reports a capture's traffic only while
+    the built sources are still the ones it measured."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in CONV_SOURCES:
+        with open(os.path.join(REPO, "finalproject-losslessimagecompression_amd", "csrc", name),
+                  "rb") as f:
+            h.update(name.encode() + b"\0" + f.read())
+    return h.hexdigest()
+
+
+def pmc_traffic(kernels, n_last: int, extra: str = "conv3_wino_reduce_kernel"):
+    """HBM bytes per launch of the DenseLayer conv from the newest committed PMC passes
     (profiles/<round>/pmc_bench/{fetch,write}.csv, written by tools/pmc_bench.sh over this
     bench), over the same launches as roofline.achieved: the process's last n_last dispatches
-    whose name contains `kernel` (the sampled encode pass ends the run) plus the `extra`
+    whose name contains one of `kernels` (the sampled encode pass ends the run) plus the `extra`
     dispatches among them (the 8x8 split-K reduce, whose time roofline_pass also counts).
     Bytes = 2 x FETCH_SIZE (the gfx950 correction for 16-B-per-lane streaming reads,
-    MI355X_MICROARCH.md "HBM") + WRITE_SIZE, KiB -> bytes.  None when no such profile exists."""
+    MI355X_MICROARCH.md "HBM") + WRITE_SIZE, KiB -> bytes.  (None, why) when no capture exists
+    or the newest one was taken from other kernel sources (its source_hash.txt differs from
+    conv_source_hash())."""
     import csv
     import glob
     fetch = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_bench", "fetch.csv")))
     if not fetch or n_last <= 0:
         return None, None
     d = os.path.dirname(fetch[-1])
+    hp = os.path.join(d, "source_hash.txt")
+    want = conv_source_hash()
+    have = open(hp).read().strip() if os.path.exists(hp) else None
+    if have != want:
+        return None, (f"{os.path.relpath(d, REPO)}: captured from other kernel sources "
+                      f"(hash {have or 'unrecorded'} != built {want[:16]}); not reported")
 
     def total(name):
         path = os.path.join(d, name)
         if not os.path.exists(path):
             return None
         rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Dispatch_Id"]))
-        main = [r for r in rows if kernel in r["Kernel_Name"]]
+        main = [r for r in rows if any(k in r["Kernel_Name"] for k in kernels)]
         if len(main) < n_last:
             return None
         d0 = int(main[-n_last]["Dispatch_Id"])
@@ -109,7 +134,7 @@ def pmc_traffic(kernel: str, n_last: int, extra: str = "conv3_wino_reduce_kernel
     f, w = total("fetch.csv"), total("write.csv")
     if f is None or w is None:
         return None, None
-    return (2.0 * f + w) * 1024.0 / n_last, os.path.relpath(d, REPO)
+    return (2.0 * f + w) * 1024.0 / n_last, f"{os.path.relpath(d, REPO)} (sources {want[:16]})"
 
 def rans_roofline(trace, bs, steps):
     """rANS encode / decode (prep + serial pass per launch pair), timed with HIP events on
@@ -144,6 +169,11 @@ def rans_roofline(trace, bs, steps):
 
 def conv_kernel_name(eng):
     from idfcodec import engine
+    if eng.wino and eng.conv_mode == "dx3":
+        return ("conv3_dx3_kernel<3, ...> at the 32x32 and 16x16 levels: DenseLayer 3x3 conv "
+                "with the 1x1 folded in, direct form, split-f16 products (x = xh + xl split once "
+                "per staged value, xh.wh + xl.wh + xh.wl on v_mfma_f32_16x16x32_f16, f32 "
+                "accumulation); conv3_wino_kernel<3, 448, true, ...> (+ split-K reduce) at 8x8")
     if eng.wino and eng.conv_mode == "x3":
         return ("conv3_wino_kernel<3, 448, true, false> (+conv3_wino_reduce_kernel at 8x8): "
                 "DenseLayer 3x3 conv with the 1x1 folded in, Winograd F(2x2,3x3), split-f16 "
@@ -161,13 +191,26 @@ def conv_kernel_name(eng):
 
 
 def wino_exec_ratio(eng):
-    """MFMA FLOPs executed per algorithmic (direct-conv) FLOP of the 3x3 conv: Winograd
-    F(2x2,3x3) issues 16 products per 2x2 outputs instead of 36, over 16-padded outputs
-    (43 real growth channels -> 48).  1.0 for the direct kernels."""
+    """MFMA FLOPs executed per algorithmic (direct-conv) FLOP of the 3x3 conv, FLOP-weighted over
+    the levels.  Winograd F(2x2,3x3) issues 16 products per 2x2 outputs instead of 36 (x3: as
+    three K=16 f16 MFMA passes); dx3 issues 14 K=32 MFMAs per 16 channels x 16 pixels x 16
+    outputs where the three split products need 13.5 (the ninth tap's lo product pairs with
+    zeros); both over 16-padded outputs (43 real growth channels -> 48).  1.0 for the direct
+    f32 kernels."""
     if not eng.wino:
         return 1.0
-    r = 16.0 / 36.0 * 48.0 / 43.0
-    return 3.0 * r if eng.conv_mode == "x3" else r  # x3: three f16 MFMA passes per product
+    pad = 48.0 / 43.0
+    wino = 16.0 / 36.0 * pad
+    if eng.conv_mode == "f32":
+        return wino
+    direct = 3.0 * 14.0 / 13.5 * pad
+    num = den = 0.0
+    for l, L in enumerate(eng.levels):
+        f = L.h * L.w * sum(b.geom.flops_per_pixel(True) for b in eng.couple[l] + [eng.prior[l]])
+        dx = eng.conv_mode == "dx3" and eng._dx3_level(l)
+        num += f * (direct if dx else 3.0 * wino)
+        den += f
+    return num / den
 
 
 def _cpu_model() -> str:
@@ -397,9 +440,11 @@ def conv_algorithmic_bytes(eng, B):
         cached = L.prior_x_zero and not eng.conditional
         for geom in [b.geom for b in eng.couple[l]] + ([] if cached else [eng.prior[l].geom]):
             c = geom.a
+            # weights per (c, g): 16 Winograd positions or 9 direct taps, as f16 (hi, lo) pairs
+            npos = 9 if (eng.conv_mode == "dx3" and eng._dx3_level(l)) else 16
             for g in geom.growth:
                 n += 1
-                byt += 4 * P * (c + g) + 16 * c * g * 4
+                byt += 4 * P * (c + g) + npos * c * g * 4
                 c += g
     return n, byt
 
@@ -566,14 +611,15 @@ def main():
     _lib.lib().idf_timer_destroy(timer)
 
     flops = eng.flops_per_image()["total"]
-    # both range-check variants of the kernel: roofline_pass times every DenseLayer conv launch
-    kname = ("conv3_wino_kernel<3, 448, true," if eng.conv_mode == "x3"
-             else "conv3_wino_kernel<3, 448, false")
-    traffic, traffic_src = pmc_traffic(kname, c3_n) if eng.wino else (None, None)
+    # both range-check variants of the kernels: roofline_pass times every DenseLayer conv launch
+    knames = {"dx3": ("conv3_dx3_kernel<3,", "conv3_wino_kernel<3, 448, true,"),
+              "x3": ("conv3_wino_kernel<3, 448, true,",),
+              "f32": ("conv3_wino_kernel<3, 448, false",)}[eng.conv_mode] if eng.wino else ()
+    traffic, traffic_src = pmc_traffic(knames, c3_n) if eng.wino else (None, None)
     n_algo, b_algo = conv_algorithmic_bytes(eng, B)
     algo_bytes = b_algo / n_algo if n_algo == c3_n and n_algo else None
-    # the x3 kernel's products run on f16 MFMA: price them against the f16 dense peak
-    peak = PEAK_F16_TFLOPS if (eng.wino and eng.conv_mode == "x3") else PEAK_F32_TFLOPS
+    # the split-f16 kernels' products run on f16 MFMA: price them against the f16 dense peak
+    peak = PEAK_F16_TFLOPS if (eng.wino and eng.conv_mode in ("x3", "dx3")) else PEAK_F32_TFLOPS
     flops_exec = eng.flops_per_image(fold=eng.fold)["total"]
     fold, conv_mode, kdesc, exec_ratio = eng.fold, eng.conv_mode, conv_kernel_name(eng), \
         wino_exec_ratio(eng)

@@ -1345,11 +1345,6 @@ static int wino_launch(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
   g.vec4 = ((uintptr_t)out % 16 == 0) && (ld_out % 4 == 0);
   if (vtap && (!bfull || ldv < N)) return IDF_ERR_ARG;
   if (res && ld_res < N) return IDF_ERR_ARG;
-  if (x3 && !res && !IDF_WINO_STAMPS && wq_enabled()) {
-    const int rc = wq_launch(stream, B, H, W, C, x, ld_x, (const uint16_t*)u, nft, yscale, b3,
-                             vtap, ldv, bfull, N, out, ld_out, act, slope, flag, check_in);
-    if (rc != IDF_ERR_UNSUPPORTED) return rc;
-  }
   if (IDF_WINO_STAMPS) g.part = workspace;
   if (pl.ksplit > 1) {
     g.ldp = (N + 3) / 4 * 4;

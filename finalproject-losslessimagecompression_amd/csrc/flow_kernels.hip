@@ -637,6 +637,13 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
                                       blk->b3[i], blk->vtap[i], blk->ldv, blk->bfull[i],
                                       blk->g_pad, feat + c, ld_feat, f16 + c, ld16, n16,
                                       blk->act, blk->slope, ws, ws_floats)
+               : (blk->wx3 && blk->dx3 && blk->dx3_w[i] &&
+                  idf_conv3x3_dx3_supported(H, W, blk->g_pad))
+                   ? idf_conv3x3_dx3(stream, B, H, W, c, feat, ld_feat, blk->dx3_w[i],
+                                     (blk->g_pad + 15) / 16, blk->dx3_yscale[i], blk->b3[i],
+                                     blk->vtap[i], blk->ldv, blk->bfull[i], blk->g_pad, feat + c,
+                                     ld_feat, blk->act, blk->slope, blk->range_flag,
+                                     i == 0 ? 1 : 0)
                : (wino && blk->wx3 && blk->wx3_u[i])
                    ? idf_conv3x3_wx3(stream, B, H, W, c, feat, ld_feat, blk->wx3_u[i],
                                      blk->wino_nft, blk->wx3_yscale[i], blk->b3[i], blk->vtap[i],

@@ -1,5 +1,5 @@
-// wino_common.h -- helpers shared by the Winograd F(2x2,3x3) conv kernels (conv3_wino.hip,
-// conv3_wk.hip): tile planning, halo pitch, B^T rows, fast index division, activations.
+// wino_common.h -- helpers shared by the 3x3 conv kernels (conv3_wino.hip, conv3_dx3.hip):
+// tile planning, halo pitch, B^T rows, fast index division, activations.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -134,15 +134,5 @@ static inline WinoPlan wino_plan(int H, int W, int nslab, int N) {
   pl.ok = 1;
   return pl;
 }
-
-// The "wq" kernel (conv3_wq.hip): the split-f16 Winograd conv with each wave owning all 16
-// transform positions of its tiles.  IDF_ERR_UNSUPPORTED when the geometry / mode is outside
-// its scope (the caller then runs wx3).  Arguments as idf_conv3x3_wx3.
-int wq_launch(void* stream, int32_t B, int32_t H, int32_t W, int32_t C, const float* x,
-              int64_t ld_x, const uint16_t* u, int32_t nft, float yscale, const float* b3,
-              const float* vtap, int32_t ldv, const float* bfull, int32_t N, float* out,
-              int64_t ld_out, int32_t act, float slope, uint32_t* flag, int32_t check_input);
-// wx3 launches go to wq where it applies when IDF_WQ=1 (read once per process)
-bool wq_enabled();
 
 }  // namespace idf

@@ -55,6 +55,7 @@ class IdfDenseBlock(ctypes.Structure):
         ("halo", i32), ("wino", i32), ("wino_nft", i32), ("wino_u", P * MAX_DEPTH),
         ("bf16", i32), ("wb16", P * MAX_DEPTH),
         ("wx3", i32), ("wx3_yscale", f32 * MAX_DEPTH), ("wx3_u", P * MAX_DEPTH), ("range_flag", P),
+        ("dx3", i32), ("dx3_yscale", f32 * MAX_DEPTH), ("dx3_w", P * MAX_DEPTH),
     ]
 
 
@@ -110,14 +111,9 @@ SIGNATURES = {
                                        i32, P, i64, i32, f32, P, i32, P, i64]),
     "idf_conv3x3_wx3_res": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, f32, P, i32, P,
                                            i64, P, i64, i32, f32, P, i32, P, i64]),
-    "idf_conv3x3_wk_supported": (ctypes.c_int, [i32, i32]),
-    "idf_conv3x3_wk_workspace": (i64, [i32, i32, i32, i32, i32]),
-    "idf_conv3x3_wq": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, f32, P, P, i32, P,
-                                      i32, P, i64, i32, f32, P, i32]),
-    "idf_conv3x3_wk": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, f32, P, P, i32, P,
-                                      i32, P, i64, i32, f32, P, i32, P, i64]),
-    "idf_conv3x3_wk_res": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, f32, P, i32, P,
-                                          i64, P, i64, i32, f32, P, i32, P, i64]),
+    "idf_conv3x3_dx3_supported": (ctypes.c_int, [i32, i32, i32]),
+    "idf_conv3x3_dx3": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, f32, P, P, i32, P,
+                                       i32, P, i64, i32, f32, P, i32]),
     "idf_conv3x3_bf16_workspace": (i64, [i32, i32, i32, i32, i32]),
     "idf_conv3x3_bf16": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, P, P, i32, P, i32,
                                         P, i64, P, i64, i32, i32, f32, P, i64]),

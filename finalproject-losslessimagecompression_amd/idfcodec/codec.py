@@ -31,7 +31,9 @@ FLAG_CONV_X3 = 1
 # must run the same one.  Version 1 wrote 0 both for exact-f32 Winograd and for every engine
 # that predates the field (halo / gemm / unfold / bf16): a version-1 file with flags 0 reads as
 # conv "unrecorded", which any engine but a split-f16 one may decode (the pre-field behaviour).
-CONV_CODES = {"f32": 0, "x3": 1, "halo": 2, "gemm": 3, "unfold": 4, "bf16": 5}
+CONV_CODES = {"f32": 0, "x3": 1, "halo": 2, "gemm": 3, "unfold": 4, "bf16": 5, "dx3": 6}
+# the split-f16 / exact-f32 modes one engine switches between per bitstream (engine.CONV_MODES)
+SWITCHABLE = ("dx3", "x3", "f32")
 CONV_NAMES = {v: k for k, v in CONV_CODES.items()}
 
 
@@ -47,12 +49,24 @@ class Bitstream:
     status: torch.Tensor | None = None
     meta: dict = field(default_factory=dict)
     # host (CPU int64) copy of nwords when the producer already had one (encode's compaction,
-    # from_bytes, the multi-GPU exchanges): sizes and checks then never wait on the device
+    # from_bytes, the multi-GPU exchanges): sizes and checks then never wait on the device.
+    # It must equal nwords: assigning nwords drops it (the next nwords_host() reads the device
+    # table again), and a copy whose length differs from nwords is dropped at construction.
     host_nwords: torch.Tensor | None = None
+
+    def __post_init__(self):
+        hn = self.host_nwords
+        if hn is not None and hn.numel() != self.nwords.numel():
+            object.__setattr__(self, "host_nwords", None)
+
+    def __setattr__(self, name, value):
+        object.__setattr__(self, name, value)
+        if name == "nwords" and "host_nwords" in self.__dict__:
+            object.__setattr__(self, "host_nwords", None)  # a new table: its host copy is stale
 
     def nwords_host(self) -> torch.Tensor:
         """nwords on the host: the kept copy, else one device->host read (cached)."""
-        if self.host_nwords is None:
+        if self.host_nwords is None or self.host_nwords.numel() != self.nwords.numel():
             self.host_nwords = self.nwords.detach().to("cpu", torch.int64)
         return self.host_nwords
 
@@ -438,7 +452,7 @@ class ImageCodec:
         produced the streams is recorded in the bitstream (meta['conv'], container flag)."""
         eng = self.engine
         mode = eng.conv_family
-        if mode == "x3":
+        if mode in ("x3", "dx3"):
             eng.clear_range_flag()
         nl = 1
         if lanes_img is not None and cond is None and not eng.conditional:
@@ -471,14 +485,14 @@ class ImageCodec:
             ws = load()
             eng.forward_pm(B, cond=cond)
             bs = self.coder.encode(ws, B, compact=compact)
-        if mode == "x3" and eng.range_flag_tripped():
+        if mode in ("x3", "dx3") and eng.range_flag_tripped():
             eng.set_conv_mode("f32")
             try:
                 ws = load()
                 eng.forward_pm(B, cond=cond)
                 bs = self.coder.encode(ws, B, compact=compact)
             finally:
-                eng.set_conv_mode("x3")
+                eng.set_conv_mode(mode)
             mode = "f32"
         bs.meta["conv"] = mode
         return bs
@@ -549,15 +563,15 @@ class ImageCodec:
                                  f"{bs.words.numel()} present")
         conv, have = bs.meta.get("conv", "f32"), eng.conv_family
         if conv == "unrecorded":  # version-1 file, flags 0: any engine but split-f16
-            if have == "x3":
+            if have in ("x3", "dx3"):
                 raise ValueError("bitstream predates the conv field (version 1, flags 0) and "
                                  "was not coded with split-f16 convs; decode it with "
                                  "engine.set_conv_mode('f32') or the engine that wrote it")
             return
         if conv not in CONV_CODES:
             raise ValueError(f"unknown conv mode {conv!r}")
-        switchable = conv in ("x3", "f32") and have in ("x3", "f32") and (conv == "f32" or
-                                                                          eng.wx3)
+        switchable = conv in SWITCHABLE and have in SWITCHABLE and (
+            conv == "f32" or (conv == "x3" and eng.wx3) or (conv == "dx3" and eng.dx3))
         if conv != have and not switchable:
             raise ValueError(f"bitstream was coded with {conv!r} convs; this engine runs "
                              f"{have!r} (IDF_FOLD / IDF_WINO / IDF_HALO / precision differ): "
@@ -594,7 +608,7 @@ class ImageCodec:
         off = [sum(sz[:i]) for i in range(nl)]
         # the convs must run as the encoder ran them (bit-identical couplings)
         mode, prev = bs.meta.get("conv", "f32"), eng.conv_mode
-        if mode not in ("x3", "f32"):  # a fixed family, checked equal in check_bitstream
+        if mode not in SWITCHABLE:  # a fixed family, checked equal in check_bitstream
             mode = prev
         if mode != prev:
             eng.set_conv_mode(mode)

@@ -24,6 +24,7 @@ With backend "nccl" every tensor must live on the rank's GPU; the CPU tests use 
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 import torch.distributed as dist
@@ -173,11 +174,16 @@ def host_group(group=None):
     collective over the world)."""
     if dist.get_backend(group) == dist.Backend.GLOO and not SEPARATE_HOST_GROUP:
         return group
-    key = None if group is None else id(group)
-    g = _HOST_GROUPS.get(key)
-    if g is None:
-        ranks = None if group is None else dist.get_process_group_ranks(group)
-        g = _HOST_GROUPS[key] = dist.new_group(ranks=ranks, backend="gloo")
+    # keyed by the group's ranks and checked against the group object itself (a weak
+    # reference): a destroyed group, or a re-initialised world, never hands out the gloo
+    # group of its predecessor even if the new group object reuses the old one's id()
+    pg = group if group is not None else dist.distributed_c10d._get_default_group()
+    ranks = tuple(dist.get_process_group_ranks(pg))
+    hit = _HOST_GROUPS.get(ranks)
+    if hit is not None and hit[0]() is pg:
+        return hit[1]
+    g = dist.new_group(ranks=None if group is None else list(ranks), backend="gloo")
+    _HOST_GROUPS[ranks] = (weakref.ref(pg), g)
     return g
 
 

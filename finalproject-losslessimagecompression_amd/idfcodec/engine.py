@@ -28,6 +28,7 @@ from ._lib import IdfDenseBlock, IdfHeadOut, check, lib, ptr
 from .packing import PackedBlock, pack_dense_block, round_up
 
 FLOAT = 4
+CONV_MODES = ("dx3", "x3", "f32")
 # Fold each DenseLayer's 1x1 conv into its 3x3 conv (packing.fold_layer): -46% of the
 # flow FLOPs at imagenet64; IDF_FOLD=0 runs the reference's two convolutions instead.
 FOLD = os.environ.get("IDF_FOLD", "1") != "0"
@@ -41,6 +42,10 @@ WINO = os.environ.get("IDF_WINO", "1") != "0"
 # hi/lo pair, three f16 MFMAs, f32 accumulation -- fp32-class error) with a
 # range guard that falls back to the exact-f32 kernel; IDF_WX3=0 always uses the latter.
 WX3 = os.environ.get("IDF_WX3", "1") != "0"
+# ... and, where the geometry allows (images a multiple of 16 wide: conv3_dx3.hip), as the direct
+# conv on the same split-f16 products with no transform ("dx3", the default mode); IDF_DX3=0 keeps
+# every layer on wx3.  Conv modes: 'dx3' (dx3 where supported, wx3 elsewhere), 'x3', 'f32'.
+DX3 = os.environ.get("IDF_DX3", "1") != "0"
 
 
 class DeviceBlock:
@@ -61,6 +66,7 @@ class DeviceBlock:
         self.wino_u = [dev(a) for a in packed.wino_u]
         self.wb16 = [dev(a.view(np.int16)) for a in packed.wb16]
         self.wx3_u = [dev(a.view(np.int16)) for a in packed.wx3_u]
+        self.dx3_w = [dev(a.view(np.int16)) for a in packed.dx3_w]
         d = IdfDenseBlock()
         g = self.geom
         d.depth = g.depth
@@ -99,6 +105,10 @@ class DeviceBlock:
         for i, u in enumerate(self.wx3_u):
             d.wx3_u[i] = u.data_ptr()
             d.wx3_yscale[i] = packed.wx3_yscale[i]
+        d.dx3 = 1 if (d.wx3 and self.dx3_w) else 0
+        for i, w in enumerate(self.dx3_w):
+            d.dx3_w[i] = w.data_ptr()
+            d.dx3_yscale[i] = packed.dx3_yscale[i]
         d.bf16 = 1 if (packed.fold and self.wb16) else 0
         for i, u in enumerate(self.wb16):
             d.wb16[i] = u.data_ptr()
@@ -175,6 +185,9 @@ class FlowEngine:
             lib().idf_conv3x3_wino_supported(model.H // s, model.W // s)
             for s in [model.blocks[0]["extend"].scale ** (l + 1) for l in range(model.nsplit)])
         self.wx3 = self.wino and WX3
+        self.dx3 = self.wx3 and DX3 and any(
+            lib().idf_conv3x3_dx3_supported(model.H // s, model.W // s, 48)
+            for s in [model.blocks[0]["extend"].scale ** (l + 1) for l in range(model.nsplit)])
         # device word the wx3 range guard ORs into (see IdfDenseBlock.range_flag)
         self.range_flag = torch.zeros(1, dtype=torch.int32, device=self.device)
         sd = {k: v for k, v in model.state_dict().items()}
@@ -214,12 +227,14 @@ class FlowEngine:
         for l in range(self.nsplit):
             self.couple.append([DeviceBlock(pack_dense_block(
                 sd, f"blocks.{l}.flows.{2 * k + 1}.dense.", c_depth, c_act, fold=self.fold,
-                wino=self.wino, bf16=self.precision == "bf16", wx3=self.wx3),
+                wino=self.wino, bf16=self.precision == "bf16", wx3=self.wx3,
+                dx3=self.dx3 and self._dx3_level(l)),
                 self.device) for k in range(self.nflows)])
             self.prior.append(DeviceBlock(pack_dense_block(sd, f"blocks.{l}.prior.NN.", p_depth,
                                                            p_act, fold=self.fold, wino=self.wino,
                                                            bf16=self.precision == "bf16",
-                                                           wx3=self.wx3),
+                                                           wx3=self.wx3,
+                                                           dx3=self.dx3 and self._dx3_level(l)),
                                           self.device))
             ids_l, inv_l = [], []
             for k in range(self.nflows + 1):
@@ -243,7 +258,7 @@ class FlowEngine:
         self._blocks = blocks
         for b in blocks:
             b.desc.range_flag = self.range_flag.data_ptr()
-        self.conv_mode = "x3" if self.wx3 else "f32"
+        self.conv_mode = "dx3" if self.dx3 else ("x3" if self.wx3 else "f32")
         self.ld_feat = max(b.geom.ld_feat for b in blocks)
         # tmp: split-K partials (f32); bf16 blocks also keep their bf16 feature shadow at its
         # front (pitch round_up(k, 64) bf16 = half as many floats) ahead of 2-way partials
@@ -254,25 +269,35 @@ class FlowEngine:
         self._top_prior = None
 
     # ------------------------------------------------------------ conv mode
+    def _dx3_level(self, l: int) -> bool:
+        Lv = self.levels[l]
+        return bool(lib().idf_conv3x3_dx3_supported(Lv.h, Lv.w, 48))
+
     def set_conv_mode(self, mode: str):
-        """'x3' (split-f16 Winograd, needs wx3 weights) or 'f32' (exact-f32 Winograd).  The
-        decoder must run the mode the encoder ran (Bitstream.meta['conv'])."""
-        if mode not in ("x3", "f32"):
-            raise ValueError(f"conv mode must be 'x3' or 'f32', not {mode!r}")
+        """'dx3' (split-f16 direct conv where the geometry allows, split-f16 Winograd
+        elsewhere), 'x3' (split-f16 Winograd everywhere; both need the split weights) or 'f32'
+        (exact-f32 Winograd).  The decoder must run the mode the encoder ran
+        (Bitstream.meta['conv'])."""
+        if mode not in CONV_MODES:
+            raise ValueError(f"conv mode must be one of {CONV_MODES}, not {mode!r}")
         if mode == "x3" and not self.wx3:
             raise ValueError("this engine has no split-f16 (wx3) weights")
-        on = 1 if mode == "x3" else 0
+        if mode == "dx3" and not self.dx3:
+            raise ValueError("this engine has no split-f16 direct-conv (dx3) weights")
+        on = 1 if mode in ("x3", "dx3") else 0
         for b in self._blocks:
             b.desc.wx3 = on if b.wx3_u else 0
+            b.desc.dx3 = 1 if (mode == "dx3" and b.dx3_w and b.desc.wx3) else 0
         self.conv_mode = mode
         self._top_prior = None  # computed under the previous mode
 
     @property
     def conv_family(self) -> str:
         """Which conv arithmetic produces the couplings -- the decoder must run the same one
-        (Bitstream.meta['conv']): 'x3' / 'f32' (Winograd split-f16 / exact f32, switchable
-        per bitstream), 'bf16', 'halo' (direct LDS-halo kernel), 'gemm' (folded implicit
-        GEMM) or 'unfold' (the reference's 1x1 + 3x3, IDF_FOLD=0)."""
+        (Bitstream.meta['conv']): 'dx3' / 'x3' / 'f32' (split-f16 direct + Winograd / split-f16
+        Winograd / exact-f32 Winograd, switchable per bitstream), 'bf16', 'halo' (direct
+        LDS-halo kernel), 'gemm' (folded implicit GEMM) or 'unfold' (the reference's 1x1 +
+        3x3, IDF_FOLD=0)."""
         if self.precision == "bf16":
             return "bf16"
         if not self.fold:

@@ -114,6 +114,8 @@ class PackedBlock:
     wb16: list = field(default_factory=list)    # fold+bf16: bf16_weights() per layer (uint16)
     wx3_u: list = field(default_factory=list)   # fold+wino+wx3: wino_weights_x3() per layer
     wx3_yscale: list = field(default_factory=list)
+    dx3_w: list = field(default_factory=list)    # fold+dx3: dx3_weights() per layer (uint16)
+    dx3_yscale: list = field(default_factory=list)
 
 
 def fold_layer(w1, b1, w3):
@@ -196,29 +198,31 @@ def x3_scale(U: np.ndarray) -> int:
     return max(-14, min(k, 60))
 
 
-def wk_weights(w: np.ndarray, U: np.ndarray | None = None):
-    """Split-f16 Winograd weights for idf_conv3x3_wk (conv3_wk.hip: three K=32 f16 MFMAs per
-    32-channel slab).  U = G g G^T in float64 (wino_transform64, channels zero-padded to a
-    multiple of 32), scaled by 2^k (x3_scale, the same k as wino_weights_x3), split
-    Uh = f16(U'), Ul = f16(U' - Uh).  Returns (uint16 [16 positions][nslab][nft][2: hi, lo]
-    [64 lanes][8], yscale = 2^-k) where lane = 16*q + r holds outputs 16*f + r, channels
-    32*slab + 8*q .. +7 -- the B operand of v_mfma_f32_16x16x32_f16 for k-group q."""
-    if U is None:
-        U = wino_transform64(w, (w.shape[2] + 15) // 16)
-    n_alloc, c16 = U.shape[1], U.shape[2]
+def dx3_weights(w: np.ndarray, C: int):
+    """Split-f16 direct-conv weights for idf_conv3x3_dx3 (conv3_dx3.hip).
+
+    w: [n_alloc, 9, ldw] folded 3x3 weights (float64 preferred) in the padded channel
+    coordinates, C = the layer's padded input channels.  Scaled by 2^k (x3_scale: max |w| 2^k
+    in [2^14, 2^15)) and split wh = f16(w'), wl = f16(w' - wh), both round-to-nearest-even.
+    Returns (uint16 [nslab][2: hi, lo][9 taps][nft][16 out][16 ch], yscale = 2^-k): per slab
+    the A-operand (output-row) fragments the kernel stages into LDS verbatim; channels at or
+    past C are zero."""
+    n_alloc = w.shape[0]
+    assert n_alloc % 16 == 0
     nft = n_alloc // 16
-    nslab = (c16 + 31) // 32
-    Up = np.zeros((16, n_alloc, nslab * 32), np.float64)
-    Up[:, :, :c16] = U
-    k = x3_scale(Up)
-    Us = Up * (2.0 ** k)
-    hi = Us.astype(np.float16)
-    lo = (Us - hi.astype(np.float64)).astype(np.float16)
-    out = np.empty((16, nslab, nft, 2, 4, 16, 8), np.uint16)  # pos, slab, f, hi/lo, q, r, e
+    nslab = (C + 15) // 16
+    wp = np.zeros((n_alloc, 9, nslab * 16), np.float64)
+    cw = min(C, w.shape[2])
+    wp[:, :, :cw] = w[:, :, :cw]
+    k = x3_scale(wp)
+    ws = wp * (2.0 ** k)
+    hi = ws.astype(np.float16)
+    lo = (ws - hi.astype(np.float64)).astype(np.float16)
+    out = np.empty((nslab, 2, 9, nft, 16, 16), np.uint16)
     for t, part in enumerate((hi, lo)):
-        p = part.view(np.uint16).reshape(16, nft, 16, nslab, 4, 8)  # pos, f, r, slab, q, e
-        out[:, :, :, t] = p.transpose(0, 3, 1, 4, 2, 5)
-    return np.ascontiguousarray(out.reshape(16, nslab, nft, 2, 64, 8)), float(2.0 ** -k)
+        p = part.view(np.uint16).reshape(nft, 16, 9, nslab, 16)  # f, r, tap, slab, c
+        out[:, t] = p.transpose(3, 2, 0, 1, 4)
+    return np.ascontiguousarray(out), float(2.0 ** -k)
 
 
 def bf16_weights(w: np.ndarray, C: int) -> np.ndarray:
@@ -247,10 +251,11 @@ def interior_bias(b3: np.ndarray, v: np.ndarray) -> np.ndarray:
 
 def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
                      slope: float = 0.01, fold: bool = False, wino: bool = False,
-                     bf16: bool = False, wx3: bool = False) -> PackedBlock:
+                     bf16: bool = False, wx3: bool = False, dx3: bool = False) -> PackedBlock:
     """Pack the reference DenseBlock parameters found under `prefix` in `sd`
     (keys `{prefix}layers.{i}.layers.{0,1}.{weight,bias}`, head `{prefix}layers.{depth}.*`).
-    fold=True folds each layer's 1x1 conv into its 3x3 conv (fold_layer)."""
+    fold=True folds each layer's 1x1 conv into its 3x3 conv (fold_layer); dx3=True also packs
+    the split-f16 direct-conv weights (dx3_weights) of every folded layer."""
     def arr(k):
         v = sd[prefix + k]
         if hasattr(v, "detach"):
@@ -265,7 +270,7 @@ def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
     geom = BlockGeometry(a=a, depth=depth, growth=gs, n_head=n_head)
     g_alloc = round_up(geom.g_pad, tile_n(geom.g_pad))
     w1s, b1s, w3s, b3s, n1s, ld1s, ld3s = [], [], [], [], [], [], []
-    vts, bfs, wus, wbs, wxs, wys = [], [], [], [], [], []
+    vts, bfs, wus, wbs, wxs, wys, wds, wdy = [], [], [], [], [], [], [], []
     c = a
     for i in range(depth):
         k = geom.k_in[i]
@@ -290,9 +295,14 @@ def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
             wf64, v64 = fold_layer64(w1, b1, w3)
             wf, v = wf64.astype(np.float32), v64.astype(np.float32)
             w3p[:g][:, :, pos] = wf
-            if wino:
+            if wino or dx3:
                 w64 = np.zeros((g_alloc, 9, ldw3), np.float64)
                 w64[:g][:, :, pos] = wf64
+            if dx3:
+                wd, yd = dx3_weights(w64, k)
+                wds.append(wd)
+                wdy.append(yd)
+            if wino:
                 U64 = wino_transform64(w64, ldw3 // 16)
                 wus.append(wino_weights(w64, ldw3 // 16, U64))
                 if wx3:
@@ -323,7 +333,7 @@ def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
     bhp = np.zeros(nh_alloc, np.float32)
     bhp[:n_head] = arr(f"layers.{depth}.bias")
     return PackedBlock(geom, act, slope, fold, vts, bfs, w1s, b1s, w3s, b3s, whp, bhp, g_alloc,
-                       n1s, ld1s, ld3s, nh_alloc, ldwh, wus, wbs, wxs, wys)
+                       n1s, ld1s, ld3s, nh_alloc, ldwh, wus, wbs, wxs, wys, wds, wdy)
 
 
 def unpack_features(feat: np.ndarray, geom: BlockGeometry, n: int) -> np.ndarray:

@@ -193,6 +193,13 @@ typedef struct IdfDenseBlock {
   float wx3_yscale[IDF_MAX_DEPTH];
   const uint16_t *wx3_u[IDF_MAX_DEPTH];
   uint32_t *range_flag;
+  /* dx3 = 1 (with wx3 = 1): layers with dx3_w[i] whose geometry idf_conv3x3_dx3_supported
+   * takes run the split-f16 direct conv (idf_conv3x3_dx3, weights dx3_w[i], yscale
+   * dx3_yscale[i], the same range guard); other geometries keep wx3.  The choice depends on
+   * (H, W, g_pad) only, so an encoder and its decoder make it alike. */
+  int32_t dx3;
+  float dx3_yscale[IDF_MAX_DEPTH];
+  const uint16_t *dx3_w[IDF_MAX_DEPTH];
 } IdfDenseBlock;
 
 /* Head epilogue target */
@@ -317,44 +324,24 @@ int idf_conv3x3_wx3_res(void *stream, int32_t B, int32_t H, int32_t W, int32_t C
                         float slope, uint32_t *d_flag, int32_t check_input,
                         float *d_workspace, int64_t workspace_floats);
 
-/* "wq": the same split-f16 Winograd conv (same products, U layout, range guard and arguments
- * as idf_conv3x3_wx3), each wave owning all 16 transform positions of 16 tiles so that the
- * output transform stays in registers (conv3_wq.hip).  Scope: one K split, N a multiple of 48
- * after rounding to 16 (3 n-fragments per block), tile widths 32 and 16 (32x32 and 16x16
- * images and wider); IDF_ERR_UNSUPPORTED otherwise.  idf_conv3x3_wx3 itself runs this kernel
- * wherever it applies (unless the environment sets IDF_WQ=0), so the engine's encoder and
- * decoder agree; the outputs differ from wx3's own kernel in the last bits (another fixed
- * summation order).  Replaces the reference's DenseLayer conv (nnlayer.py:48-51, 1x1 folded
- * in, nnblock.py:53-56). */
-int idf_conv3x3_wq(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, const float *d_x,
-                   int64_t ld_x, const uint16_t *d_u, int32_t nft, float yscale,
-                   const float *d_b3, const float *d_vtap, int32_t ldv, const float *d_bfull,
-                   int32_t N, float *d_out, int64_t ld_out, int32_t act, float slope,
-                   uint32_t *d_flag, int32_t check_input);
-
-/* "wk": the same split-f16 Winograd convs (same products, same 1e-5 contract, same range
- * guard and arguments as idf_conv3x3_wx3 / _wx3_res) with all three products on K=32 MFMAs
- * (v_mfma_f32_16x16x32_f16, 32-channel slabs, one wave per SIMD; conv3_wk.hip).  d_u: uint16
- * [16 positions][ceil(C/32) slabs][nft][hi, lo][64 lanes][8] (idfcodec/packing.py wk_weights).
- * Replaces the reference's DenseLayer conv (nnlayer.py:48-51, 1x1 folded in) and the VQ-VAE
- * 3x3 convs (nnblock.py:59-84).  Every geometry idf_conv3x3_wino_supported takes except the
- * packed-small-image stage (idf_conv3x3_wk_supported: 4x4 / 2x2 images stay on wx3); the
- * outputs differ from wx3's in the last bits (another fixed summation order), so an encoder
- * and its decoder must run the same one. */
-int idf_conv3x3_wk_supported(int32_t H, int32_t W);
-int64_t idf_conv3x3_wk_workspace(int32_t B, int32_t H, int32_t W, int32_t C, int32_t N);
-int idf_conv3x3_wk(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, const float *d_x,
-                   int64_t ld_x, const uint16_t *d_u, int32_t nft, float yscale,
-                   const float *d_b3, const float *d_vtap, int32_t ldv, const float *d_bfull,
-                   int32_t N, float *d_out, int64_t ld_out, int32_t act, float slope,
-                   uint32_t *d_flag, int32_t check_input, float *d_workspace,
-                   int64_t workspace_floats);
-int idf_conv3x3_wk_res(void *stream, int32_t B, int32_t H, int32_t W, int32_t C,
-                       const float *d_x, int64_t ld_x, const uint16_t *d_u, int32_t nft,
-                       float yscale, const float *d_bias, int32_t N, float *d_out,
-                       int64_t ld_out, const float *d_res, int64_t ld_res, int32_t act,
-                       float slope, uint32_t *d_flag, int32_t check_input,
-                       float *d_workspace, int64_t workspace_floats);
+/* "dx3": the same folded DenseLayer 3x3 conv in direct form with the split-f16 products of
+ * wx3 -- x = xh + xl (split once as the halo is staged), w' = w * 2^k = wh + wl (host float64),
+ * x.w' ~= xh.wh + xl.wh + xh.wl with f32 accumulation, then * yscale = 2^-k -- all on
+ * v_mfma_f32_16x16x32_f16 with no transform and no VALU in the k-loop (conv3_dx3.hip).
+ * d_w: uint16 [ceil(C/16) slabs][2: hi, lo][9 taps][nft][16 outputs][16 channels]
+ * (idfcodec/packing.py dx3_weights), nft = ceil(N/16) <= 3.  Geometry: W a multiple of 16
+ * (idf_conv3x3_dx3_supported; 16x16 output tiles, any H).  d_out 16-B aligned, ld_out a
+ * multiple of 4.  Range guard as idf_conv3x3_wx3 (|y| >= 8192 or NaN on a stored output; with
+ * check_input, |x| >= 32768 or NaN on an input).  The outputs differ from wx3's in the last
+ * bits (another fixed summation order), so an encoder and its decoder run the same one
+ * (Bitstream conv code 'dx3').  Replaces the reference's DenseLayer conv (nnlayer.py:48-51,
+ * 1x1 folded in, nnblock.py:53-56). */
+int idf_conv3x3_dx3_supported(int32_t H, int32_t W, int32_t N);
+int idf_conv3x3_dx3(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, const float *d_x,
+                    int64_t ld_x, const uint16_t *d_w, int32_t nft, float yscale,
+                    const float *d_b3, const float *d_vtap, int32_t ldv, const float *d_bfull,
+                    int32_t N, float *d_out, int64_t ld_out, int32_t act, float slope,
+                    uint32_t *d_flag, int32_t check_input);
 
 /* The same folded 3x3 conv on bf16 MFMA (v_mfma_f32_16x16x32_bf16, fp32 accumulation).
  * The input is the bf16 shadow d_x16 of the fp32 feature columns (ld_x16 a multiple of 8,

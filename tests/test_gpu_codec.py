@@ -110,33 +110,39 @@ def test_coder_api_chained_round_trip(golden):
 
 
 def test_conv_modes_and_range_guard_fallback(monkeypatch):
-    """imagenet64 runs the split-f16 Winograd convs (conv 'x3'); a bitstream records the
-    conv mode, the decoder follows it whatever mode the engine is in, and a tripped range
-    guard re-encodes the batch with the exact-f32 convs."""
+    """imagenet64 runs the split-f16 direct convs where the geometry allows (conv 'dx3': the
+    32x32 and 16x16 levels; the 8x8 level keeps split-f16 Winograd); a bitstream records the
+    conv mode, the decoder follows it whatever mode the engine is in (dx3 / x3 / f32), and a
+    tripped range guard re-encodes the batch with the exact-f32 convs."""
     from idfcodec import synthetic
     from idfcodec.codec import Bitstream
     model = _imagenet64()
     codec = model.codec()
     eng = model.engine()
-    assert eng.conv_mode == "x3"
+    assert eng.conv_mode == "dx3"
     img = synthetic.images(4, seed=77).cuda()
+    bs_dx3 = codec.encode(img)
+    assert bs_dx3.meta["conv"] == "dx3"
+    eng.set_conv_mode("x3")
     bs_x3 = codec.encode(img)
     assert bs_x3.meta["conv"] == "x3"
     eng.set_conv_mode("f32")
     bs_f32 = codec.encode(img)
     assert bs_f32.meta["conv"] == "f32"
-    eng.set_conv_mode("x3")
-    # the modes give (slightly) different couplings, so different streams, both lossless
-    assert not (torch.equal(bs_x3.states, bs_f32.states) and torch.equal(bs_x3.words, bs_f32.words))
-    for bs in (bs_x3, bs_f32, Bitstream.from_bytes(bs_f32.to_bytes(), "cuda"),
-               Bitstream.from_bytes(bs_x3.to_bytes(), "cuda")):
+    eng.set_conv_mode("dx3")
+    # the modes give (slightly) different couplings, so different streams, all lossless
+    for a_, b_ in ((bs_dx3, bs_x3), (bs_x3, bs_f32), (bs_dx3, bs_f32)):
+        assert not (torch.equal(a_.states, b_.states) and torch.equal(a_.words, b_.words))
+    for bs in (bs_dx3, bs_x3, bs_f32, Bitstream.from_bytes(bs_f32.to_bytes(), "cuda"),
+               Bitstream.from_bytes(bs_x3.to_bytes(), "cuda"),
+               Bitstream.from_bytes(bs_dx3.to_bytes(), "cuda")):
         out, info = codec.decode(bs)
         assert info["ok"] and torch.equal(out.cpu(), img.cpu()), bs.meta
-    assert eng.conv_mode == "x3"
+        assert eng.conv_mode == "dx3"
     # guard tripped -> exact-f32 re-encode, identical to an f32-mode encode
     monkeypatch.setattr(type(eng), "range_flag_tripped", lambda self: True)
     bs_fb = codec.encode(img)
-    assert bs_fb.meta["conv"] == "f32" and eng.conv_mode == "x3"
+    assert bs_fb.meta["conv"] == "f32" and eng.conv_mode == "dx3"
     assert torch.equal(bs_fb.states, bs_f32.states) and torch.equal(bs_fb.words, bs_f32.words)
 
 
@@ -148,4 +154,4 @@ def test_range_guard_clean_on_real_batch():
     eng = model.engine()
     eng.clear_range_flag()
     bs = codec.encode(synthetic.images(64, seed=5).cuda())
-    assert bs.meta["conv"] == "x3" and not eng.range_flag_tripped()
+    assert bs.meta["conv"] == "dx3" and not eng.range_flag_tripped()

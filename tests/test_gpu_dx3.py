@@ -1,0 +1,166 @@
+"""GPU parity of the split-f16 direct conv (idf_conv3x3_dx3, conv3_dx3.hip) against fp64 conv2d
+with the same folded weights: the 1e-5 bound of the flow contract, fp32-class error (within a
+small factor of the exact-f32 Winograd kernel's own), the range guard, data far from unit scale,
+and determinism (the same bits for an image coded alone or inside a batch)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def scaled_err(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).abs() / b.abs().clamp(min=1.0)).max().item()
+
+
+def make_case(B, H, W, C, N, fold, scale=1.0, spike=None, seed=None):
+    from idfcodec.packing import round_up
+    g = torch.Generator().manual_seed(seed if seed is not None else B * 7 + H * 3 + C)
+    ld = round_up(C + N, 16) + 4
+    X = torch.randn(B * H * W, ld, generator=g) * scale
+    if spike is not None:
+        X[B * H * W // 2, 0] = spike
+    ldw = round_up(C, 16)
+    n_alloc = round_up(N, 16)
+    Wt = torch.randn(n_alloc, 9, ldw, generator=g, dtype=torch.float64) / np.sqrt(9 * C)
+    Wt[N:] = 0.0
+    b3 = torch.randn(n_alloc, generator=g) * 0.1
+    vt = torch.randn(9, n_alloc, generator=g) * 0.1 if fold else None
+    bfull = None
+    if fold:
+        s = b3.clone()
+        for t in range(9):
+            s = s + vt[t]
+        bfull = s
+    return dict(B=B, H=H, W=W, C=C, N=N, ld=ld, X=X, Wt=Wt, b3=b3, vt=vt, bfull=bfull,
+                n_alloc=n_alloc, ldw=ldw)
+
+
+def run_dx3(cs, act, check_in=1, X=None, B=None):
+    from idfcodec import _lib
+    from idfcodec._lib import check, lib, ptr
+    from idfcodec.packing import dx3_weights
+    B = cs["B"] if B is None else B
+    X = cs["X"] if X is None else X
+    H, W, C, N, ld, n_alloc = cs["H"], cs["W"], cs["C"], cs["N"], cs["ld"], cs["n_alloc"]
+    dev = torch.device("cuda")
+    Wd, ysc = dx3_weights(cs["Wt"].numpy(), C)
+    Wdd = torch.from_numpy(Wd.view(np.int16)).to(dev)
+    Xd, b3d = X.to(dev), cs["b3"].to(dev)
+    vtd = cs["vt"].to(dev) if cs["vt"] is not None else None
+    bfd = cs["bfull"].to(dev) if cs["bfull"] is not None else None
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    out = torch.zeros(B * H * W, ld, device=dev)
+    check(lib().idf_conv3x3_dx3(_lib.stream_ptr(), B, H, W, C, ptr(Xd), ld, ptr(Wdd), n_alloc // 16,
+                                ysc, ptr(b3d), ptr(vtd), n_alloc, ptr(bfd), N, ptr(out), ld,
+                                _lib.ACT[act], 0.01, ptr(flag), check_in), "dx3")
+    torch.cuda.synchronize()
+    return out.cpu(), int(flag.item())
+
+
+def run_wino_f32(cs, act):
+    from idfcodec import _lib
+    from idfcodec._lib import check, lib, ptr
+    from idfcodec.packing import wino_weights
+    B, H, W, C, N, ld, n_alloc = (cs[k] for k in ("B", "H", "W", "C", "N", "ld", "n_alloc"))
+    dev = torch.device("cuda")
+    U = torch.from_numpy(wino_weights(cs["Wt"].numpy(), cs["ldw"] // 16)).to(dev)
+    vtd = cs["vt"].to(dev) if cs["vt"] is not None else None
+    bfd = cs["bfull"].to(dev) if cs["bfull"] is not None else None
+    wsn = lib().idf_conv3x3_wino_workspace(B, H, W, C, N)
+    ws = torch.empty(max(wsn, 1), device=dev)
+    out = torch.zeros(B * H * W, ld, device=dev)
+    check(lib().idf_conv3x3_wino(_lib.stream_ptr(), B, H, W, C, ptr(cs["X"].to(dev)), ld, ptr(U),
+                                 n_alloc // 16, ptr(cs["b3"].to(dev)), ptr(vtd), n_alloc, ptr(bfd), N,
+                                 ptr(out), ld, _lib.ACT[act], 0.01, ptr(ws), wsn), "wino")
+    torch.cuda.synchronize()
+    return out.cpu()
+
+
+def reference(cs, act):
+    B, H, W, C, N = cs["B"], cs["H"], cs["W"], cs["C"], cs["N"]
+    x4 = cs["X"][:, :C].double().view(B, H, W, C).permute(0, 3, 1, 2)
+    w4 = cs["Wt"][:N, :, :C].permute(0, 2, 1).reshape(N, C, 3, 3)
+    ref = F.conv2d(x4, w4, padding=1) + cs["b3"][:N].double().view(1, -1, 1, 1)
+    if cs["vt"] is not None:
+        mask = F.conv2d(torch.ones(1, 1, H, W, dtype=torch.float64),
+                        torch.eye(9, dtype=torch.float64).view(9, 1, 3, 3), padding=1)
+        ref = ref + torch.einsum("tn,bthw->bnhw", cs["vt"][:, :N].double(), mask)
+    if act == "ReLU":
+        return F.relu(ref)
+    if act == "LeakyReLU":
+        return F.leaky_relu(ref, 0.01)
+    return ref
+
+
+def got_nchw(out, cs):
+    B, H, W, N = cs["B"], cs["H"], cs["W"], cs["N"]
+    return out[:, :N].double().view(B, H, W, N).permute(0, 3, 1, 2)
+
+
+@pytest.mark.parametrize("B,H,W,C,N,act,fold", [
+    (3, 32, 32, 52, 44, "ReLU", True), (5, 16, 16, 100, 44, "ReLU", True),
+    (3, 32, 32, 496, 44, "ReLU", True), (1, 16, 16, 520, 44, "ReLU", True),
+    (2, 64, 64, 8, 16, "LeakyReLU", True), (2, 20, 32, 24, 32, "ReLU", True),
+    (2, 16, 48, 12, 43, "LeakyReLU", True), (1, 5, 16, 40, 44, "ReLU", True),
+    (4, 16, 16, 36, 12, "ReLU", False), (2, 32, 32, 100, 48, "LeakyReLU", True),
+    (3, 17, 16, 20, 44, "None", True)])
+def test_dx3_vs_fp64(B, H, W, C, N, act, fold):
+    cs = make_case(B, H, W, C, N, fold)
+    out, flag = run_dx3(cs, act)
+    ref = reference(cs, act)
+    e = scaled_err(got_nchw(out, cs), ref)
+    e32 = scaled_err(got_nchw(run_wino_f32(cs, act), cs), ref)
+    print(f"dx3 {e:.2e} f32-wino {e32:.2e}")
+    assert flag == 0
+    assert torch.all(out[:, N:] == 0), "wrote outside the N output columns"
+    assert e <= 1e-5, f"dx3 max scaled error {e:.3e}"
+    assert e <= max(4 * e32, 1e-6), (e32, e)
+
+
+@pytest.mark.parametrize("scale", [1e-3, 30.0])
+def test_dx3_far_from_unit_scale(scale):
+    cs = make_case(2, 16, 16, 200, 44, True, scale=scale)
+    out, flag = run_dx3(cs, "ReLU")
+    ref = reference(cs, "ReLU")
+    e = scaled_err(got_nchw(out, cs), ref)
+    e32 = scaled_err(got_nchw(run_wino_f32(cs, "ReLU"), cs), ref)
+    assert flag == 0
+    assert e <= max(4 * e32, 1e-6), (e32, e)
+
+
+def test_dx3_batch_invariant():
+    """An image's outputs are the same bits alone and inside a batch (the decoder recomputes
+    the encoder's couplings on other batch compositions)."""
+    cs = make_case(5, 32, 32, 140, 44, True, seed=11)
+    full, _ = run_dx3(cs, "ReLU", check_in=0)
+    P = 32 * 32
+    one = cs["X"][3 * P: 4 * P].clone()
+    alone, _ = run_dx3(cs, "ReLU", check_in=0, X=one, B=1)
+    assert torch.equal(full[3 * P: 4 * P], alone)
+
+
+def test_dx3_range_guard_sets_flag():
+    for spike, want in ((40000.0, 1), (float("nan"), 1), (1000.0, 0)):
+        cs = make_case(1, 16, 16, 16, 16, True, spike=spike)
+        _, flag = run_dx3(cs, "ReLU")
+        assert flag == want, (spike, flag)
+
+
+def test_dx3_output_guard_sets_flag():
+    cs = make_case(1, 16, 16, 16, 16, True, scale=4000.0)
+    _, flag = run_dx3(cs, "None", check_in=0)
+    assert flag == 1
+    cs = make_case(1, 16, 16, 16, 16, True, scale=100.0)
+    _, flag = run_dx3(cs, "None", check_in=0)
+    assert flag == 0
+
+
+def test_dx3_unsupported_geometry():
+    from idfcodec._lib import lib
+    assert lib().idf_conv3x3_dx3_supported(32, 32, 44) == 1
+    assert lib().idf_conv3x3_dx3_supported(8, 8, 44) == 0
+    assert lib().idf_conv3x3_dx3_supported(27, 23, 32) == 0
+    assert lib().idf_conv3x3_dx3_supported(16, 16, 64) == 0

@@ -49,7 +49,8 @@ def in64():
     from idfcodec import configs, synthetic
     model = synthetic.build_model(configs.get("imagenet64")).cuda()
     eng = model.engine()
-    assert eng.conv_mode == "x3" and eng.wx3, "imagenet64 must run the split-f16 Winograd convs"
+    assert eng.conv_mode == "dx3" and eng.wx3 and eng.dx3, \
+        "imagenet64 must run the split-f16 convs (direct at 32x32 / 16x16, Winograd at 8x8)"
     return model, eng
 
 
@@ -82,18 +83,30 @@ def _layer_out(feat, geom, i):
     return feat[:, c0:c0 + geom.growth[i]]
 
 
+@pytest.mark.parametrize("mode", ["dx3", "x3"])
 @pytest.mark.parametrize("lvl", [0, 1, 2])
-def test_imagenet64_x3_blocks_teacher_forced(in64, lvl):
-    """Every DenseBlock of level `lvl` as the engine packed it (x3 mode)."""
+def test_imagenet64_x3_blocks_teacher_forced(in64, lvl, mode):
+    """Every DenseBlock of level `lvl` as the engine packed it, in both split-f16 modes: 'dx3'
+    (the default: the direct conv at the 32x32 and 16x16 levels, Winograd at 8x8) and 'x3'
+    (Winograd everywhere)."""
     import flow_oracle as FO
     from idfcodec.modules import run_device_block
     model, eng = in64
+    eng.set_conv_mode(mode)
+    try:
+        _x3_blocks_teacher_forced(model, eng, lvl, mode, FO, run_device_block)
+    finally:
+        eng.set_conv_mode("dx3")
+
+
+def _x3_blocks_teacher_forced(model, eng, lvl, mode, FO, run_device_block):
     Lv = eng.levels[lvl]
     hw = Lv.h
     g = torch.Generator().manual_seed(100 + lvl)
     worst_block = worst_layer = 0.0
     for name, mod, db in _blocks(model, eng, lvl):
-        assert db.desc.wino and db.desc.wx3, (name, "not on the split-f16 Winograd path")
+        assert db.desc.wino and db.desc.wx3, (name, "not on the split-f16 path")
+        assert db.desc.dx3 == (1 if mode == "dx3" and Lv.w % 16 == 0 else 0), (name, mode)
         c_in = mod.i_channel
         x = _grid((2, c_in, hw, hw), g)
         sd = {k: v.detach().cpu() for k, v in mod.state_dict().items()}
@@ -116,7 +129,7 @@ def test_imagenet64_x3_blocks_teacher_forced(in64, lvl):
         assert torch.equal(again, out), (name, "re-run differs")
         one, _ = run_device_block(db, x[1:2].contiguous().cuda())
         assert torch.equal(one, out[1:2]), (name, "image 1 alone differs from inside the batch")
-    print(f"level {lvl}: worst whole-block {worst_block:.2e}, worst layer {worst_layer:.2e}")
+    print(f"{mode} level {lvl}: worst whole-block {worst_block:.2e}, worst layer {worst_layer:.2e}")
 
 
 def test_imagenet64_x3_blocks_realistic_inputs(in64):

@@ -1,7 +1,7 @@
 """Kernel microbenchmark of the folded 3x3 conv at the imagenet64 shapes (B=256): the LDS
 halo-tiled kernel (idf_conv3x3_halo) and the implicit-GEMM kernel (idf_conv3x3_fold_f32),
 per level and layer width.  Prints achieved TFLOP/s (unpadded FLOPs).
-Env filters: KB_ONLY=wino,halo,gemm,bf16  KB_LEVELS=0,1,2  KB_LAYERS=0,3,6,9,11  KB_REPS=10."""
+Env filters: KB_ONLY=wino,wx3,dx3,halo,gemm,bf16  KB_LEVELS=0,1,2  KB_LAYERS=0,3,6,9,11  KB_REPS=10."""
 import os
 import sys
 
@@ -33,7 +33,7 @@ def main():
     dev = torch.device("cuda")
     s = _lib.stream_ptr()
     g_pad, g_alloc, g_real = 44, 48, 43
-    only = os.environ.get("KB_ONLY", "wino,wx3,wk,halo,gemm,bf16").split(",")
+    only = os.environ.get("KB_ONLY", "wino,wx3,dx3,halo,gemm,bf16").split(",")
     layers = [int(v) for v in os.environ.get("KB_LAYERS", "0,3,6,9,11").split(",")]
     levels = [int(v) for v in os.environ.get("KB_LEVELS", "0,1,2").split(",")]
     reps = int(os.environ.get("KB_REPS", "10"))
@@ -84,17 +84,14 @@ def main():
                                             ptr(feat) + c_pad * 4, ld, 0, 0.0, ptr(flag), 0, ptr(wws),
                                             wwn), "wx3")
 
-            from idfcodec.packing import wk_weights
-            UK, ksc = wk_weights(np.random.default_rng(0).normal(0, 0.01, (g_alloc, 9, ldw)))
-            UK = torch.from_numpy(UK.view(np.int16)).to(dev)
-            kwn = lib().idf_conv3x3_wk_workspace(B, hw, hw, c_pad, g_pad)
-            kws = torch.empty(max(kwn, 1), device=dev)
+            from idfcodec.packing import dx3_weights
+            WD, dsc = dx3_weights(np.random.default_rng(0).normal(0, 0.01, (g_alloc, 9, ldw)), c_pad)
+            WD = torch.from_numpy(WD.view(np.int16)).to(dev)
 
-            def wk():
-                check(lib().idf_conv3x3_wk(s, B, hw, hw, c_pad, ptr(feat), ld, ptr(UK), g_alloc // 16,
-                                           ksc, ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
-                                           ptr(feat) + c_pad * 4, ld, 0, 0.0, ptr(flag), 0, ptr(kws),
-                                           kwn), "wk")
+            def dx3():
+                check(lib().idf_conv3x3_dx3(s, B, hw, hw, c_pad, ptr(feat), ld, ptr(WD), g_alloc // 16,
+                                            dsc, ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
+                                            ptr(feat) + c_pad * 4, ld, 0, 0.0, ptr(flag), 0), "dx3")
 
             from idfcodec.packing import bf16_weights
             WB = torch.from_numpy(bf16_weights(np.random.default_rng(1).normal(
@@ -117,7 +114,7 @@ def main():
                                                  g_alloc, ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
                                                  ptr(feat) + c_pad * 4, ld, 0, 0.0), "gemm")
             line = f"L{lvl} hw={hw:2d} c={c_pad:4d} P={P:7d}"
-            for name, fn in (("wino", wino), ("wx3", wx3), ("wk", wk), ("halo", halo), ("gemm", gemm),
+            for name, fn in (("wino", wino), ("wx3", wx3), ("dx3", dx3), ("halo", halo), ("gemm", gemm),
                              ("bf16", bf16)):
                 if name not in only:
                     continue

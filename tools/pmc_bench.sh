@@ -18,4 +18,7 @@ run() {
 }
 run fetch FETCH_SIZE
 run write WRITE_SIZE
+# the kernel sources these counters describe: bench.py reports the traffic only while the
+# built sources hash the same (bench.conv_source_hash)
+python3 -c "import bench; print(bench.conv_source_hash())" > gpurun_out/pmc_bench/source_hash.txt
 echo done
