@@ -13,9 +13,9 @@
 //   rans_encode     : pass 2 (rans.pyx:61-66), ONE WAVE per stream: the state chain
 //                     on the scalar unit (readlane of coalesced 64-symbol record chunks,
 //                     magic-reciprocal quotient), words stored 64 at a time.
-//   rans_decode_prep: decode pass 1, fully parallel: the EXACT CDF at the last bin of
-//                     each of the 2048-bin window's 64 blocks, per symbol.
-//   rans_decode     : rans.pyx:69-110, ONE WAVE per stream.  The reference's
+//   rans_decode     : rans.pyx:69-110, ONE WAVE per stream (plus one table-producer wave
+//                     that computes, a window ahead in LDS, the EXACT CDF at the last bin
+//                     of each of the 2048-bin window's 64 blocks, per symbol).  The reference's
 //                     11-12 step binary search over the 2048-bin window is
 //                     replaced by one integer ballot of mod against the 64 exact block
 //                     boundaries and ONE round of 33 exact CDF probes over the chosen
@@ -403,71 +403,116 @@ __device__ __forceinline__ void exact_search(uint64_t mod, int lower, float mi, 
   *c_hi = __builtin_amdgcn_readlane(cq, kk);
 }
 
-// Per-symbol parameters of the decoder's fast loop, precomputed by pass 1 (32 B): twice the
-// window origin plus one, -mean and scale widened to double and the refined reciprocal of the
-// scale.
+// Per-symbol parameters of the decoder's fast loop (32 B): twice the window origin plus one,
+// -mean and scale widened to double and the refined reciprocal of the scale.
 struct DecRec {
   int32_t l2, pad;  // 2 * lower + 1
   double mneg, sd, rs;
 };
 
-// Decode pass 1 (fully parallel, off the serial chain): for every symbol the EXACT CDF at
-// the last bin of each of the window's 64 blocks of 32 bins,
-// btab[i * 64 + l] = CDF(lower_i + 32 l + 31) (scale <= 0: unused, 0), and its DecRec.
-__global__ void __launch_bounds__(256) rans_decode_prep_kernel(int64_t n, const float* __restrict__ mean,
-                                                               const float* __restrict__ scale,
-                                                               int32_t* __restrict__ btab,
-                                                               DecRec* __restrict__ rec) {
-  __shared__ uint64_t tab[32];
-  if (threadIdx.x < 32) tab[threadIdx.x] = kExp2fTab[threadIdx.x];
-  __syncthreads();
-  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t i = g >> 6;
-  const int l = (int)(g & 63);
-  if (i >= n) return;
-  const float mi = mean[i], si = scale[i];
-  const int lower = rans_lower_int(mi);
-  btab[g] = si > 0.0f ? cdf_any(lower + 32 * l + 31, lower, mi, si, tab) : 0;
-  if (l == 0) {
-    const bool fast = si > 0.0f && fast_scale_ok(si);
-    rec[i] = DecRec{2 * lower + 1, 0, -(double)mi, (double)si, fast ? rcp_refined((double)si) : 0.0};
+// The table producer of one decoded stream ("helper" wave): for every window of 64 symbols
+// (in decode order), the EXACT CDF at the last bin of each of the window's 64 blocks of 32
+// bins, bt[t * 64 + l] = CDF(lower_t + 32 l + 31) (scale <= 0: unused, 0), and the symbols'
+// DecRecs, written into the LDS slot the decoding wave reads next.  Nothing of it depends on
+// the state chain, so it runs a window ahead of the chain on another wave of the block and
+// the decode needs no device workspace: the boundaries never leave the CU.
+__device__ __forceinline__ void dec_fill_window(const float* __restrict__ mean,
+                                                const float* __restrict__ scale, int64_t i_hi,
+                                                int cnt, int lane, int32_t* bt, DecRec* rc,
+                                                const uint64_t* tab) {
+  float mv = 0.0f, sv = 1.0f;
+  if (lane < cnt) {  // lane t: symbol i_hi - t (the reverse order the chain decodes in)
+    mv = mean[i_hi - lane];
+    sv = scale[i_hi - lane];
+  }
+  const int lower_v = rans_lower_int(mv);
+  const bool fast_v = sv > 0.0f && fast_scale_ok(sv);
+  const double rs_v = fast_v ? rcp_refined((double)sv) : 0.0;
+  rc[lane] = DecRec{2 * lower_v + 1, 0, -(double)mv, (double)sv, rs_v};
+  const uint64_t rsb = __builtin_bit_cast(uint64_t, rs_v);
+  for (int t = 0; t < cnt; ++t) {
+    const int lower = __builtin_amdgcn_readlane(lower_v, t);
+    const float mi = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mv), t));
+    const float si = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, sv), t));
+    const int q = lower + 32 * lane + 31;
+    int c = 0;
+    if (si > 0.0f && fast_scale_ok(si)) {
+      const double rs = __builtin_bit_cast(
+          double, ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(rsb >> 32), t) << 32) |
+                      (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rsb, t));
+      c = cdf_bin(q, lower, (double)mi, (double)si, rs, tab);
+    } else if (si > 0.0f) {
+      c = rans_cdf(sym_x(q), mi, si, rans_lower_f(lower), tab);
+    }
+    bt[t * 64 + lane] = c;
   }
 }
 
-// WAVES streams per block, one per wave: the waves never synchronise after the table
-// load, so packing them only concentrates the decode on fewer CUs (nstreams / WAVES), which
-// leaves the rest of the chip to a concurrent lane's convolutions (ImageCodec lanes).
+// The decoding wave's progress marker once it has stopped: its table producer exits
+constexpr int kDecDone = 1 << 30;
+
+// PAIRS streams per block.  Waves 0..PAIRS-1 decode one stream each (the serial chain);
+// wave PAIRS + p fills stream p's window tables (dec_fill_window) one window ahead, through
+// a two-slot LDS ring and two LDS counters per pair (ready: windows filled, consumed: windows
+// decoded; workgroup-scope release/acquire).  The decoding waves never synchronise with each
+// other, so packing PAIRS streams per block only concentrates the decode on fewer CUs
+// (nstreams / PAIRS), which leaves the rest of the chip to a concurrent lane's convolutions
+// (ImageCodec lanes).
 //
 // Per symbol (rans.pyx:84-109), for scale > 0 in the fast range:
-//   1. one integer ballot of mod against the 64 exact block boundaries (pass 1) gives the
-//      block b of the reference's answer: the first block whose last bin has CDF > mod, or
-//      b = 64 when none has (then s = lower + 2048, rans.pyx's loop exit);
+//   1. one integer ballot of mod against the 64 exact block boundaries gives the block b of
+//      the reference's answer: the first block whose last bin has CDF > mod, or b = 64 when
+//      none has (then s = lower + 2048, rans.pyx's loop exit);
 //   2. ONE exact round: lane j evaluates the CDF at q = lower + 32 b - 1 + j (lanes 1..32
 //      the block, lane 0 its left neighbour); the CDF is strictly increasing for scale > 0
 //      (part2 steps by one, part1 is monotone: glibc expf verified monotone on every float),
 //      so the first lane in 1..32 with CDF > mod (or q past the window) is s, and lanes k-1,
 //      k hold CDF(s - 1), CDF(s) -- no bracket checks and no second search.
 // Other scales take the reference's own searches (exact_search, ref_binary_search).
-template <int WAVES>
-__global__ void __launch_bounds__(64 * WAVES) rans_decode_kernel(
+template <int PAIRS>
+__global__ void __launch_bounds__(128 * PAIRS) rans_decode_kernel(
     int64_t nstreams, const int64_t* __restrict__ sym_off, const int64_t* __restrict__ word_off,
     const int64_t* __restrict__ nwords, const uint32_t* __restrict__ words,
     const float* __restrict__ mean, const float* __restrict__ scale,
     const uint64_t* __restrict__ init_state, uint64_t* __restrict__ final_state,
-    float* __restrict__ out, int32_t* __restrict__ status, const int32_t* __restrict__ btab,
-    const DecRec* __restrict__ rec) {
+    float* __restrict__ out, int32_t* __restrict__ status) {
   __shared__ uint64_t tab[32];
-  // block boundaries and parameter records, 2 windows per wave
+  // block boundaries and parameter records, 2 windows per stream
   // (one spare row each: the fast loop reads one symbol ahead unconditionally)
-  __shared__ __attribute__((aligned(16))) int32_t bt_all[WAVES][2][65 * 64];
-  __shared__ __attribute__((aligned(16))) DecRec rc_all[WAVES][2][65];
+  __shared__ __attribute__((aligned(16))) int32_t bt_all[PAIRS][2][65 * 64];
+  __shared__ __attribute__((aligned(16))) DecRec rc_all[PAIRS][2][65];
+  __shared__ int ready[PAIRS], consumed[PAIRS];
   if (threadIdx.x < 32) tab[threadIdx.x] = kExp2fTab[threadIdx.x];
+  if (threadIdx.x < PAIRS) {
+    ready[threadIdx.x] = 0;
+    consumed[threadIdx.x] = 0;
+  }
   __syncthreads();
-  const int wave = WAVES == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t k = (int64_t)blockIdx.x * WAVES + wave;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int pr = wave < PAIRS ? wave : wave - PAIRS;
+  const int64_t k = (int64_t)blockIdx.x * PAIRS + pr;
   if (k >= nstreams) return;
-  auto& bt = bt_all[wave];
-  auto& rc = rc_all[wave];
+  auto& bt = bt_all[pr];
+  auto& rc = rc_all[pr];
+  if (wave >= PAIRS) {  // the table producer
+    const int lane = threadIdx.x & 63;
+    const int64_t b = sym_off[k], n = sym_off[k + 1] - b;
+    int win = 0;
+    for (int64_t j0 = 0; j0 < n; j0 += 64, ++win) {
+      // slot win & 1 is free once window win - 2 is decoded
+      for (;;) {
+        const int c = __hip_atomic_load(&consumed[pr], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (c >= kDecDone) return;
+        if (c >= win - 1) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      const int cnt = n - j0 < 64 ? (int)(n - j0) : 64;
+      dec_fill_window(mean, scale, b + n - 1 - j0, cnt, lane, bt[win & 1], rc[win & 1], tab);
+      __hip_atomic_store(&ready[pr], win + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return;
+  }
+  __builtin_amdgcn_s_setprio(2);  // the chain's instructions first on a SIMD shared with a producer
   const int lane = threadIdx.x & 63;
   const int64_t b = sym_off[k], n = sym_off[k + 1] - b;
   const uint32_t* w = words + word_off[k];
@@ -487,25 +532,6 @@ __global__ void __launch_bounds__(64 * WAVES) rans_decode_kernel(
     if (j0 + lane < n) {
       mv = mean[i];
       sv = scale[i];
-    }
-  };
-  // window at j0 -> bt[slot][t * 64 + l] = btab[(i_hi - t) * 64 + l], i_hi = b + n - 1 - j0,
-  // rc[slot][t] = rec[i_hi - t]
-  auto ld_blk = [&](int64_t j0, int slot) {
-    const int cnt = n - j0 < 64 ? (int)(n - j0) : 64;
-    for (int m = 0; m < 2; ++m) {  // 32 records (1 KiB) per DMA wave-instruction, 2 lanes each
-      const int tl = 32 * m + (lane >> 1);
-      const int64_t i = b + n - 1 - j0 - (tl < cnt ? tl : cnt - 1);
-      __builtin_amdgcn_global_load_lds((const void*)((const char*)(rec + i) + 16 * (lane & 1)),
-                                       (__attribute__((address_space(3))) void*)(&rc[slot][32 * m]),
-                                       16, 0, 0);
-    }
-    for (int t = 0; t < cnt; t += 4) {  // 4 symbols (1 KiB) per DMA wave-instruction
-      const int tl = t + (lane >> 4);
-      const int64_t i = b + n - 1 - j0 - (tl < cnt ? tl : cnt - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(btab + i * 64 + 4 * (lane & 15)),
-                                       (__attribute__((address_space(3))) void*)(&bt[slot][t * 64]),
-                                       16, 0, 0);
     }
   };
   // Words: a 128-word register buffer (lane l of wA holds w[wb - 1 - l], of wB w[wb - 65 - l])
@@ -545,17 +571,18 @@ __global__ void __launch_bounds__(64 * WAVES) rans_decode_kernel(
   float mcur, scur, mnxt = 0.0f, snxt = 1.0f;
   ld_params(0, mcur, scur);
   asm volatile("" ::"v"(wA), "v"(wB), "v"(mcur), "v"(scur));
-  if (n > 0) ld_blk(0, 0);
   bool stop = false;
-  int slot = 0;
-  for (int64_t j0 = 0; j0 < n && !stop; j0 += 64, slot ^= 1) {
+  int slot = 0, win = 0;
+  for (int64_t j0 = 0; j0 < n && !stop; j0 += 64, slot ^= 1, ++win) {
     const int cnt = n - j0 < 64 ? (int)(n - j0) : 64;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // boundaries, parameters, words landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // parameters and words landed
+    // this window's boundaries and records are in LDS slot `slot` once ready > win
+    while (__hip_atomic_load(&ready[pr], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= win)
+      __builtin_amdgcn_s_sleep(1);
     wA = wnA;  // j0 = 0: the same buffer
     wB = wnB;
     wb = wnb;
     if (j0 + 64 < n) {
-      ld_blk(j0 + 64, slot ^ 1);
       ld_params(j0 + 64, mnxt, snxt);
       ld_words(pos, wnA, wnB);
       wnb = pos;
@@ -724,7 +751,10 @@ __global__ void __launch_bounds__(64 * WAVES) rans_decode_kernel(
     if (lane < done) out[b + n - 1 - j0 - lane] = outv;
     mcur = mnxt;
     scur = snxt;
+    // window win decoded: its slot may be refilled (the release orders this window's LDS reads)
+    __hip_atomic_store(&consumed[pr], win + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
+  __hip_atomic_store(&consumed[pr], kDecDone, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   if (lane == 0) {
     final_state[k] = state;
     status[k] = flag | (pos > 0 ? IDF_STREAM_WORDS_LEFT : 0);
@@ -857,13 +887,16 @@ int idf_rans_encode_streams(void* stream, int64_t nstreams, int64_t nsym, const 
 
 // Streams per block: 4 by default (a quarter of the CUs: decode lanes run beside another
 // lane's convs; alone it measures the same as 1), IDF_DECODE_WPB=1 for one per block.
-static int decode_waves_per_block() {
+static int decode_pairs_per_block() {
   const char* e = getenv("IDF_DECODE_WPB");
   return (e && atoi(e) == 1) ? 1 : 4;
 }
 
+// The block-boundary tables live in LDS only (rans_decode_kernel's producer waves): the
+// decode needs no device workspace.  A nonzero size keeps callers' allocations well-formed.
 int64_t idf_rans_decode_workspace_bytes(int64_t nsym) {
-  return (64 * (int64_t)sizeof(int32_t) + (int64_t)sizeof(DecRec)) * (nsym > 0 ? nsym : 1);
+  (void)nsym;
+  return 256;
 }
 
 int idf_rans_decode_streams(void* stream, int64_t nstreams, int64_t nsym, const int64_t* sym_off,
@@ -873,20 +906,16 @@ int idf_rans_decode_streams(void* stream, int64_t nstreams, int64_t nsym, const 
                             int64_t workspace_bytes) {
   if (nstreams < 0 || nsym < 0) return IDF_ERR_ARG;
   if (nstreams == 0) return IDF_OK;
+  (void)workspace;
   if (workspace_bytes < idf_rans_decode_workspace_bytes(nsym)) return IDF_ERR_WORKSPACE;
-  int32_t* btab = (int32_t*)workspace;
-  DecRec* rec = (DecRec*)(btab + 64 * (nsym > 0 ? nsym : 1));
-  if (nsym > 0)
-    hipLaunchKernelGGL(rans_decode_prep_kernel, dim3((unsigned)((nsym * 64 + 255) / 256)), dim3(256),
-                       0, (hipStream_t)stream, nsym, mean, scale, btab, rec);
-  if (decode_waves_per_block() == 4)
-    hipLaunchKernelGGL(rans_decode_kernel<4>, dim3((unsigned)((nstreams + 3) / 4)), dim3(256), 0,
+  if (decode_pairs_per_block() == 4)
+    hipLaunchKernelGGL(rans_decode_kernel<4>, dim3((unsigned)((nstreams + 3) / 4)), dim3(512), 0,
                        (hipStream_t)stream, nstreams, sym_off, word_off, nwords, words, mean,
-                       scale, init_state, final_state, out, status, btab, rec);
+                       scale, init_state, final_state, out, status);
   else
-    hipLaunchKernelGGL(rans_decode_kernel<1>, dim3((unsigned)nstreams), dim3(64), 0,
+    hipLaunchKernelGGL(rans_decode_kernel<1>, dim3((unsigned)nstreams), dim3(128), 0,
                        (hipStream_t)stream, nstreams, sym_off, word_off, nwords, words, mean,
-                       scale, init_state, final_state, out, status, btab, rec);
+                       scale, init_state, final_state, out, status);
   return idf_last_error();
 }
 

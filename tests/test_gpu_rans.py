@@ -256,3 +256,64 @@ def test_decoder_part1_short_chain_exhaustive():
     bad = torch.zeros(1, dtype=torch.int64, device="cuda")
     check(lib().idf_rans_part1_selfcheck(_lib.stream_ptr(), 0, 1 << 32, ptr(bad)), "part1")
     assert int(bad.item()) == 0
+
+
+def test_decode_stream_stopping_early_leaves_neighbours_exact(oracle):
+    """A stream whose decode stops on a zero scale (rans.pyx:36 raises ZeroDivisionError) ends
+    its table producer early; the other streams of its block (4 per block) decode on, equal to
+    the oracle."""
+    g = np.random.default_rng(12)
+    lens = np.array([300, 700, 130, 900, 64, 65, 1000, 5], np.int64)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    n = int(off[-1])
+    mean = (g.integers(-256, 257, n) / 256).astype(np.float32)
+    scale = (np.exp(10 * g.random(n) - 5) / 256).astype(np.float32)
+    x = (np.round((mean + scale * (10 * g.random(n) - 5)) * 256) / 256).astype(np.float32)
+    fs, words, nw, st = _enc_streams(off, x, mean, scale)
+    scale_d = scale.copy()
+    stop = {1: 5, 3: 400, 6: 64}  # stream -> decode step (the chain runs backwards) hit by scale 0
+    for k, t in stop.items():
+        scale_d[off[k + 1] - 1 - t] = 0.0
+    dfs, out, dst = _dec_streams(off, off[:-1], nw, words, mean, scale_d, fs)
+    for k in range(lens.size):
+        a, e = off[k], off[k + 1]
+        if k in stop:
+            assert dst[k] & 1, (k, dst[k])  # IDF_STREAM_SCALE_ZERO
+            t = stop[k]
+            assert np.array_equal(out[e - t:e], x[e - t:e]), k  # the symbols before the stop
+        else:
+            assert dst[k] == 0 and dfs[k] == 1 << 32, k
+            assert np.array_equal(out[a:e], x[a:e]), k
+
+
+@pytest.mark.timeout(600)
+def test_reference_scale_50m_symbols(oracle):
+    """rans/test.py at its own scale: ONE encode() and ONE decode() call of 50M symbols through
+    the reference's Python API (lists in, lists out, decode's reversed conventions), with
+    test.py's input distribution.  Encode is bit-identical to the C oracle (final state and
+    every word); decode restores the message exactly and returns the initial state.  The
+    decode keeps its block-boundary tables in LDS: no per-symbol device workspace."""
+    import time
+    from idfcodec._lib import lib
+    from rans.rans import decode, encode
+    n = 50_000_000
+    g = np.random.default_rng(50)
+    mean = (g.integers(-256, 257, n) / 256).astype(np.float32)
+    scale = (np.exp(10 * g.random(n) - 5) / 256).astype(np.float32)
+    msg = (np.round((mean + scale * (10 * g.random(n) - 5)) * 256) / 256).astype(np.float32)
+    ml, sl, xl = mean.tolist(), scale.tolist(), msg.tolist()
+    assert lib().idf_rans_decode_workspace_bytes(n) <= 64 * 1024
+    t0 = time.time()
+    st, buf = encode(1 << 32, n, xl, ml, sl)
+    t1 = time.time()
+    rst, rwords = oracle.encode(1 << 32, msg, mean, scale)
+    assert st == rst and len(buf) == rwords.size
+    assert np.array_equal(np.asarray(buf, dtype=np.uint32), rwords)
+    del rwords
+    t2 = time.time()
+    st2, rec = decode(st, buf[::-1], n, ml[::-1], sl[::-1])
+    t3 = time.time()
+    assert st2 == 1 << 32
+    assert np.array_equal(np.asarray(rec[::-1], dtype=np.float32), msg)
+    print(f"50M symbols: encode {t1 - t0:.1f} s, decode {t3 - t2:.1f} s (host lists included), "
+          f"{len(buf)} words; decode workspace {lib().idf_rans_decode_workspace_bytes(n)} B")
