@@ -74,18 +74,6 @@
 #ifndef IDF_EPI_W2
 #define IDF_EPI_W2 0
 #endif
-// X3 products: 1 = Vl.Uh (K=16) + (Vh.Uh + Vh.Ul) (one K=32 MFMA), 0 = three K=16 MFMAs.
-// Measured no faster (0.91 vs 0.90 ms over the kbench layers), so off.  Note: hipcc (ROCm
-// 7.2) emits NO wait states between a v_mfma_f32_16x16x32_f16 and a following
-// v_mfma_f32_16x16x16_f16 that reads its result as srcC, and the result is wrong
-// (tools/native: mfma_chain_probe); the K=16 -> K=32 order with the batches split by a
-// sched_barrier is the form that passes the parity tests.
-#ifndef IDF_X3_K32
-#define IDF_X3_K32 0
-#endif
-#ifndef IDF_X3_FAKE32
-#define IDF_X3_FAKE32 0
-#endif
 // XCD-aware block order (wino_common.h wino_xcd_remap): 1 = on
 #ifndef IDF_WINO_XCD
 #define IDF_WINO_XCD 1
@@ -368,49 +356,6 @@ struct WinoRole {
   template <int STEP = 0>
   __device__ __forceinline__ static void mfma_hl(const h4 (&hl)[4], const w4 (&u)[2][NF],
                                                  w4 (&acc)[NF * 2]) {
-#if IDF_X3_FAKE32
-    // timing-only (tools/native): the K=32 MFMA count of a slab-paired split-f16 scheme,
-    // 1.5 v_mfma_f32_16x16x32_f16 per (position, n-fragment) and step; results are wrong
-    {
-      const h8 a0 = __builtin_shufflevector(hl[0], hl[1], 0, 1, 2, 3, 4, 5, 6, 7);
-      const h8 a1 = __builtin_shufflevector(hl[2], hl[3], 0, 1, 2, 3, 4, 5, 6, 7);
-#pragma unroll
-      for (int jn = 0; jn < NF; ++jn) {
-        const h8 ua = __builtin_bit_cast(h8, u[0][jn]), ub = __builtin_bit_cast(h8, u[1][jn]);
-        acc[jn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, ua, acc[jn], 0, 0, 0);
-        acc[NF + jn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, ub, acc[NF + jn], 0, 0, 0);
-        if constexpr (STEP % 2 == 0) {
-          acc[jn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, ua, acc[jn], 0, 0, 0);
-          acc[NF + jn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, ub, acc[NF + jn], 0, 0, 0);
-        }
-      }
-      return;
-    }
-#endif
-    if constexpr (IDF_X3_K32) {
-      // Vl.Uh on v_mfma_f32_16x16x16_f16, then Vh.Uh + Vh.Ul as ONE
-      // v_mfma_f32_16x16x32_f16: k = 8*quad + j takes A = (Vh, Vh) against the lane's
-      // stored B fragment (Uh, Ul) -- two MFMAs instead of three, and the K=32 form runs
-      // ~1.7x the K=16 form's FLOP rate
-      const h8 a0 = __builtin_shufflevector(hl[0], hl[0], 0, 1, 2, 3, 0, 1, 2, 3);
-      const h8 a1 = __builtin_shufflevector(hl[2], hl[2], 0, 1, 2, 3, 0, 1, 2, 3);
-#pragma unroll
-      for (int jn = 0; jn < NF; ++jn) {
-        const h8 ua = __builtin_bit_cast(h8, u[0][jn]), ub = __builtin_bit_cast(h8, u[1][jn]);
-        acc[jn] = __builtin_amdgcn_mfma_f32_16x16x16f16(
-            hl[1], __builtin_shufflevector(ua, ua, 0, 1, 2, 3), acc[jn], 0, 0, 0);
-        acc[NF + jn] = __builtin_amdgcn_mfma_f32_16x16x16f16(
-            hl[3], __builtin_shufflevector(ub, ub, 0, 1, 2, 3), acc[NF + jn], 0, 0, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int jn = 0; jn < NF; ++jn) {
-        const h8 ua = __builtin_bit_cast(h8, u[0][jn]), ub = __builtin_bit_cast(h8, u[1][jn]);
-        acc[jn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, ua, acc[jn], 0, 0, 0);
-        acc[NF + jn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, ub, acc[NF + jn], 0, 0, 0);
-      }
-      return;
-    }
 #pragma unroll
     for (int p = 0; p < 3; ++p)
 #pragma unroll
@@ -932,7 +877,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
           constexpr int nvm = i == 0 ? 2 * NF : (i == 2 ? XR_PER_W : 0);
           constexpr int nst = i == 1 ? XR_PER_W : 0;
 #pragma unroll
-          for (int k = 0; k < (IDF_X3_FAKE32 ? (i % 2 == 0 ? 4 : 2) : (IDF_X3_K32 ? 4 : 6)) * NF; ++k) {
+          for (int k = 0; k < 6 * NF; ++k) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
             if (k < ND) {
               __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);

@@ -624,6 +624,21 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
     int rc = idf_f32_to_bf16_cols(stream, P, c0, (c0 + 7) / 8 * 8, feat, ld_feat, f16, ld16);
     if (rc) return rc;
   }
+  // dx3 blocks keep the split copy of their feature columns (conv3_dx3.hip) at the front of
+  // tmp: the block input is split once here, every layer writes its outputs in both forms
+  bool dx3 = blk->fold && blk->wx3 && blk->dx3 && !blk->bf16 &&
+             idf_conv3x3_dx3_supported(H, W, blk->g_pad);
+  for (int i = 0; dx3 && i < blk->depth; ++i) dx3 = blk->dx3_w[i] != nullptr;
+  uint16_t* xs = nullptr;
+  int32_t nslab_xs = 0;
+  if (dx3) {
+    nslab_xs = (int32_t)std::min<int64_t>(ld_tmp / 16, ((int64_t)blk->k_in[blk->depth] + 15) / 16);
+    if (blk->depth < 1 || nslab_xs < (blk->k_in[blk->depth - 1] + 15) / 16) return IDF_ERR_WORKSPACE;
+    xs = (uint16_t*)tmp;
+    int rc = idf_dx3_split_cols(stream, P, 0, blk->k_in[0], feat, ld_feat, xs, nslab_xs,
+                                blk->range_flag);
+    if (rc) return rc;
+  }
   for (int i = 0; i < blk->depth; ++i) {
     const int c = blk->k_in[i];
     const double cr = blk->c_real[i], gr = blk->g_real[i];
@@ -637,13 +652,11 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
                                       blk->b3[i], blk->vtap[i], blk->ldv, blk->bfull[i],
                                       blk->g_pad, feat + c, ld_feat, f16 + c, ld16, n16,
                                       blk->act, blk->slope, ws, ws_floats)
-               : (blk->wx3 && blk->dx3 && blk->dx3_w[i] &&
-                  idf_conv3x3_dx3_supported(H, W, blk->g_pad))
-                   ? idf_conv3x3_dx3(stream, B, H, W, c, feat, ld_feat, blk->dx3_w[i],
+               : dx3
+                   ? idf_conv3x3_dx3(stream, B, H, W, c, xs, nslab_xs, blk->dx3_w[i],
                                      (blk->g_pad + 15) / 16, blk->dx3_yscale[i], blk->b3[i],
                                      blk->vtap[i], blk->ldv, blk->bfull[i], blk->g_pad, feat + c,
-                                     ld_feat, blk->act, blk->slope, blk->range_flag,
-                                     i == 0 ? 1 : 0)
+                                     ld_feat, blk->act, blk->slope, blk->range_flag)
                : (wino && blk->wx3 && blk->wx3_u[i])
                    ? idf_conv3x3_wx3(stream, B, H, W, c, feat, ld_feat, blk->wx3_u[i],
                                      blk->wino_nft, blk->wx3_yscale[i], blk->b3[i], blk->vtap[i],

@@ -70,8 +70,10 @@ int idf_rans_encode_streams(void *stream, int64_t nstreams, int64_t nsym, const 
  * Words of stream k: d_words + d_word_off[k], d_nwords[k] of them in PUSH order
  * (the reference's reversed buffer_ is read from the end here); mean/scale/out
  * in natural symbol order (the reference's reversals folded into indexing).
- * nsym bounds the symbol indices (d_sym_off[nstreams] <= nsym); the workspace
- * (idf_rans_decode_workspace_bytes(nsym)) holds per-symbol search estimates. */
+ * nsym bounds the symbol indices (d_sym_off[nstreams] <= nsym).  The search tables
+ * (the exact CDF at each 32-bin block boundary of a symbol's 2048-bin window) are built in
+ * LDS by a producer wave beside each decoding wave, so the workspace
+ * (idf_rans_decode_workspace_bytes, a constant 256 B) is unused and kept for the ABI. */
 int64_t idf_rans_decode_workspace_bytes(int64_t nsym);
 int idf_rans_decode_streams(void *stream, int64_t nstreams, int64_t nsym, const int64_t *d_sym_off,
                             const int64_t *d_word_off, const int64_t *d_nwords,
@@ -193,9 +195,10 @@ typedef struct IdfDenseBlock {
   float wx3_yscale[IDF_MAX_DEPTH];
   const uint16_t *wx3_u[IDF_MAX_DEPTH];
   uint32_t *range_flag;
-  /* dx3 = 1 (with wx3 = 1): layers with dx3_w[i] whose geometry idf_conv3x3_dx3_supported
-   * takes run the split-f16 direct conv (idf_conv3x3_dx3, weights dx3_w[i], yscale
-   * dx3_yscale[i], the same range guard); other geometries keep wx3.  The choice depends on
+  /* dx3 = 1 (with wx3 = 1): a block whose geometry idf_conv3x3_dx3_supported takes runs
+   * every layer on the split-f16 direct conv (idf_conv3x3_dx3, weights dx3_w[i], yscale
+   * dx3_yscale[i], the same range guard), its split feature copy in the front of tmp; other
+   * geometries keep wx3.  The choice depends on
    * (H, W, g_pad) only, so an encoder and its decoder make it alike. */
   int32_t dx3;
   float dx3_yscale[IDF_MAX_DEPTH];
@@ -325,23 +328,33 @@ int idf_conv3x3_wx3_res(void *stream, int32_t B, int32_t H, int32_t W, int32_t C
                         float *d_workspace, int64_t workspace_floats);
 
 /* "dx3": the same folded DenseLayer 3x3 conv in direct form with the split-f16 products of
- * wx3 -- x = xh + xl (split once as the halo is staged), w' = w * 2^k = wh + wl (host float64),
- * x.w' ~= xh.wh + xl.wh + xh.wl with f32 accumulation, then * yscale = 2^-k -- all on
- * v_mfma_f32_16x16x32_f16 with no transform and no VALU in the k-loop (conv3_dx3.hip).
- * d_w: uint16 [ceil(C/16) slabs][2: hi, lo][9 taps][nft][16 outputs][16 channels]
- * (idfcodec/packing.py dx3_weights), nft = ceil(N/16) <= 3.  Geometry: W a multiple of 16
- * (idf_conv3x3_dx3_supported; 16x16 output tiles, any H).  d_out 16-B aligned, ld_out a
- * multiple of 4.  Range guard as idf_conv3x3_wx3 (|y| >= 8192 or NaN on a stored output; with
- * check_input, |x| >= 32768 or NaN on an input).  The outputs differ from wx3's in the last
- * bits (another fixed summation order), so an encoder and its decoder run the same one
- * (Bitstream conv code 'dx3').  Replaces the reference's DenseLayer conv (nnlayer.py:48-51,
- * 1x1 folded in, nnblock.py:53-56). */
+ * wx3 -- x = xh + xl, w' = w * 2^k = wh + wl (host float64), x.w' ~= xh.wh + xl.wh + xh.wl with
+ * f32 accumulation, then * yscale = 2^-k -- all on v_mfma_f32_16x16x32_f16 with no transform and
+ * no VALU in the k-loop (conv3_dx3.hip).  The input is the block's SPLIT feature copy
+ * d_xs [nslab_xs][2: hi, lo][P = B*H*W][16] f16 (idf_dx3_split_bytes bytes for 16*nslab_xs
+ * channels), staged by LDS-DMA; channels [0, C) are read.  d_w: uint16
+ * [ceil(C/16) slabs][2: hi, lo][9 taps][nft][16 outputs][16 channels] (idfcodec/packing.py
+ * dx3_weights), nft = ceil(N/16) <= 3.  Writes the N outputs as fp32 to d_out (16-B aligned,
+ * ld_out a multiple of 4) AND as split pairs to d_xs channels [C, C + N), with zeros on to the
+ * next multiple of 16 past C + N (so the next layer's last slab holds finite values).
+ * Geometry: W a multiple of 16 (idf_conv3x3_dx3_supported; 16x16 output tiles, any H).  Range
+ * guard: bit 0 of *d_flag when a stored output is NaN or |y| >= 8192.  The outputs differ from
+ * wx3's in the last bits (another fixed summation order), so an encoder and its decoder run the
+ * same one (Bitstream conv code 'dx3').  Replaces the reference's DenseLayer conv
+ * (nnlayer.py:48-51, 1x1 folded in, nnblock.py:53-56). */
 int idf_conv3x3_dx3_supported(int32_t H, int32_t W, int32_t N);
-int idf_conv3x3_dx3(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, const float *d_x,
-                    int64_t ld_x, const uint16_t *d_w, int32_t nft, float yscale,
+int64_t idf_dx3_split_bytes(int64_t P, int32_t channels);
+/* The block input's split copy: d_xs channels [c0, c1) (c0 a multiple of 16, c1 of 4) of the P
+ * fp32 rows d_x (ld_x floats), zeros for [c1, round16(c1)); bit 0 of *d_flag when an input is
+ * NaN or |x| >= 32768 (the f16 pairs' range).  Replaces nothing in the reference: the split
+ * form of the DenseBlock input (nnblock.py:53-56) the dx3 layers read. */
+int idf_dx3_split_cols(void *stream, int64_t P, int32_t c0, int32_t c1, const float *d_x,
+                       int64_t ld_x, uint16_t *d_xs, int32_t nslab_xs, uint32_t *d_flag);
+int idf_conv3x3_dx3(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, uint16_t *d_xs,
+                    int32_t nslab_xs, const uint16_t *d_w, int32_t nft, float yscale,
                     const float *d_b3, const float *d_vtap, int32_t ldv, const float *d_bfull,
                     int32_t N, float *d_out, int64_t ld_out, int32_t act, float slope,
-                    uint32_t *d_flag, int32_t check_input);
+                    uint32_t *d_flag);
 
 /* The same folded 3x3 conv on bf16 MFMA (v_mfma_f32_16x16x32_bf16, fp32 accumulation).
  * The input is the bf16 shadow d_x16 of the fp32 feature columns (ld_x16 a multiple of 8,

@@ -15,6 +15,10 @@ def scaled_err(a, b):
     return ((a - b).abs() / b.abs().clamp(min=1.0)).max().item()
 
 
+def round_up_16(v):
+    return (v + 15) // 16 * 16
+
+
 def make_case(B, H, W, C, N, fold, scale=1.0, spike=None, seed=None):
     from idfcodec.packing import round_up
     g = torch.Generator().manual_seed(seed if seed is not None else B * 7 + H * 3 + C)
@@ -38,13 +42,34 @@ def make_case(B, H, W, C, N, fold, scale=1.0, spike=None, seed=None):
                 n_alloc=n_alloc, ldw=ldw)
 
 
-def run_dx3(cs, act, check_in=1, X=None, B=None):
+F16_NAN = 0x7E00  # poison for the split buffer: every slot a layer reads must be written first
+
+
+def split_np(v):
+    """The kernels' split of fp32 values: (f16(v), f16(v - f16(v))), as uint16 bits."""
+    v = np.asarray(v, np.float32)
+    h = v.astype(np.float16)
+    lo = (v - h.astype(np.float32)).astype(np.float16)
+    return h.view(np.uint16), lo.view(np.uint16)
+
+
+def xs_channels(xs, P, nslab, c0, c1):
+    """(hi, lo) uint16 [P, c1 - c0] of the split buffer [nslab][2][P][16]."""
+    a = xs.view(nslab, 2, P, 16).permute(2, 0, 3, 1).reshape(P, nslab * 16, 2)
+    a = a[:, c0:c1].numpy().view(np.uint16)
+    return a[..., 0], a[..., 1]
+
+
+def run_dx3(cs, act, X=None, B=None, layer2=False):
+    """split_cols of the input, then one dx3 layer (or two: the second reads the first's split
+    outputs).  Returns (out, flag, xs, P, nslab_xs[, X after layer 1])."""
     from idfcodec import _lib
     from idfcodec._lib import check, lib, ptr
     from idfcodec.packing import dx3_weights
     B = cs["B"] if B is None else B
-    X = cs["X"] if X is None else X
+    X = (cs["X"] if X is None else X).clone()
     H, W, C, N, ld, n_alloc = cs["H"], cs["W"], cs["C"], cs["N"], cs["ld"], cs["n_alloc"]
+    P = B * H * W
     dev = torch.device("cuda")
     Wd, ysc = dx3_weights(cs["Wt"].numpy(), C)
     Wdd = torch.from_numpy(Wd.view(np.int16)).to(dev)
@@ -52,12 +77,33 @@ def run_dx3(cs, act, check_in=1, X=None, B=None):
     vtd = cs["vt"].to(dev) if cs["vt"] is not None else None
     bfd = cs["bfull"].to(dev) if cs["bfull"] is not None else None
     flag = torch.zeros(1, dtype=torch.int32, device=dev)
-    out = torch.zeros(B * H * W, ld, device=dev)
-    check(lib().idf_conv3x3_dx3(_lib.stream_ptr(), B, H, W, C, ptr(Xd), ld, ptr(Wdd), n_alloc // 16,
-                                ysc, ptr(b3d), ptr(vtd), n_alloc, ptr(bfd), N, ptr(out), ld,
-                                _lib.ACT[act], 0.01, ptr(flag), check_in), "dx3")
+    out = torch.zeros(P, ld, device=dev)
+    c_top = C + N + (N if layer2 else 0)
+    nslab = (c_top + 15) // 16
+    xs = torch.full((nslab * 2 * P * 16,), F16_NAN, dtype=torch.int16, device=dev)
+    assert lib().idf_dx3_split_bytes(P, nslab * 16) == xs.numel() * 2
+    s = _lib.stream_ptr()
+    check(lib().idf_dx3_split_cols(s, P, 0, C, ptr(Xd), ld, ptr(xs), nslab, ptr(flag)), "split")
+    if not layer2:
+        check(lib().idf_conv3x3_dx3(s, B, H, W, C, ptr(xs), nslab, ptr(Wdd), n_alloc // 16, ysc,
+                                    ptr(b3d), ptr(vtd), n_alloc, ptr(bfd), N, ptr(out), ld,
+                                    _lib.ACT[act], 0.01, ptr(flag)), "dx3")
+        torch.cuda.synchronize()
+        return out.cpu(), int(flag.item()), xs.cpu(), P, nslab
+    # layer 1 writes its fp32 outputs into X[:, C:C+N] and the split ones into xs
+    check(lib().idf_conv3x3_dx3(s, B, H, W, C, ptr(xs), nslab, ptr(Wdd), n_alloc // 16, ysc,
+                                ptr(b3d), ptr(vtd), n_alloc, ptr(bfd), N, ptr(Xd) + 4 * C, ld,
+                                _lib.ACT[act], 0.01, ptr(flag)), "dx3 layer 1")
+    C2 = C + N
+    W2 = torch.from_numpy(np.random.default_rng(C2).normal(0, 1 / np.sqrt(9 * C2), (n_alloc, 9, C2)))
+    W2[N:] = 0.0
+    Wd2, ysc2 = dx3_weights(W2.numpy(), C2)
+    Wdd2 = torch.from_numpy(Wd2.view(np.int16)).to(dev)
+    check(lib().idf_conv3x3_dx3(s, B, H, W, C2, ptr(xs), nslab, ptr(Wdd2), n_alloc // 16, ysc2,
+                                ptr(b3d), ptr(vtd), n_alloc, ptr(bfd), N, ptr(out), ld,
+                                _lib.ACT[act], 0.01, ptr(flag)), "dx3 layer 2")
     torch.cuda.synchronize()
-    return out.cpu(), int(flag.item())
+    return out.cpu(), int(flag.item()), xs.cpu(), P, nslab, Xd.cpu(), W2
 
 
 def run_wino_f32(cs, act):
@@ -109,7 +155,7 @@ def got_nchw(out, cs):
     (3, 17, 16, 20, 44, "None", True)])
 def test_dx3_vs_fp64(B, H, W, C, N, act, fold):
     cs = make_case(B, H, W, C, N, fold)
-    out, flag = run_dx3(cs, act)
+    out, flag, xs, P, nslab = run_dx3(cs, act)
     ref = reference(cs, act)
     e = scaled_err(got_nchw(out, cs), ref)
     e32 = scaled_err(got_nchw(run_wino_f32(cs, act), cs), ref)
@@ -118,12 +164,47 @@ def test_dx3_vs_fp64(B, H, W, C, N, act, fold):
     assert torch.all(out[:, N:] == 0), "wrote outside the N output columns"
     assert e <= 1e-5, f"dx3 max scaled error {e:.3e}"
     assert e <= max(4 * e32, 1e-6), (e32, e)
+    # the split copy: the block input as split, the layer's outputs as split, zeros after them
+    # up to the next multiple of 16 channels, nothing past it touched
+    hi, lo = xs_channels(xs, P, nslab, 0, C)
+    h_ref, l_ref = split_np(cs["X"][:, :C].numpy())
+    assert np.array_equal(hi, h_ref) and np.array_equal(lo, l_ref)
+    zend = (C + N + 15) // 16 * 16
+    hi, lo = xs_channels(xs, P, nslab, C, zend)
+    vals = np.zeros((P, zend - C), np.float32)
+    vals[:, :N] = out[:, :N].numpy()
+    h_ref, l_ref = split_np(vals)
+    assert np.array_equal(hi, h_ref) and np.array_equal(lo, l_ref)
+    if nslab * 16 > zend:
+        hi, _ = xs_channels(xs, P, nslab, zend, nslab * 16)
+        assert (hi == F16_NAN).all()
+
+
+@pytest.mark.parametrize("B,H,W,C,act", [(2, 32, 32, 52, "ReLU"), (3, 16, 16, 100, "LeakyReLU"),
+                                         (1, 16, 32, 496, "ReLU"), (2, 9, 16, 8, "ReLU")])
+def test_dx3_two_layers_through_the_split_copy(B, H, W, C, act):
+    """Layer 2 reads layer 1's split outputs (the producer side of the split copy): equal, within
+    the 1e-5 contract, to an fp64 conv of layer 1's fp32 outputs."""
+    N = 44
+    cs = make_case(B, H, W, C, N, True, seed=C + 7)
+    cs["ld"] = round_up_16(C + 2 * N) + 4
+    cs["X"] = torch.randn(B * H * W, cs["ld"], generator=torch.Generator().manual_seed(3))
+    out, flag, xs, P, nslab, X1, W2 = run_dx3(cs, act, layer2=True)
+    assert flag == 0
+    cs2 = dict(cs, C=C + N, X=X1, Wt=W2, ldw=W2.shape[2])
+    ref = reference(cs2, act)
+    e = scaled_err(got_nchw(out, cs2), ref)
+    print(f"dx3 two layers {e:.2e}")
+    assert e <= 1e-5
+    # and layer 1's fp32 outputs are what a single layer produces
+    out1, _, _, _, _ = run_dx3(cs, act)
+    assert torch.equal(X1[:, C:C + N], out1[:, :N])
 
 
 @pytest.mark.parametrize("scale", [1e-3, 30.0])
 def test_dx3_far_from_unit_scale(scale):
     cs = make_case(2, 16, 16, 200, 44, True, scale=scale)
-    out, flag = run_dx3(cs, "ReLU")
+    out, flag = run_dx3(cs, "ReLU")[:2]
     ref = reference(cs, "ReLU")
     e = scaled_err(got_nchw(out, cs), ref)
     e32 = scaled_err(got_nchw(run_wino_f32(cs, "ReLU"), cs), ref)
@@ -133,29 +214,30 @@ def test_dx3_far_from_unit_scale(scale):
 
 def test_dx3_batch_invariant():
     """An image's outputs are the same bits alone and inside a batch (the decoder recomputes
-    the encoder's couplings on other batch compositions)."""
-    cs = make_case(5, 32, 32, 140, 44, True, seed=11)
-    full, _ = run_dx3(cs, "ReLU", check_in=0)
+    the encoder's couplings on other batch compositions) -- here also across the two block
+    shapes: B = 130 (520 16x16 tiles) runs two tiles per block, B = 1 one."""
+    cs = make_case(130, 32, 32, 140, 44, True, seed=11)
+    full = run_dx3(cs, "ReLU")[0]
     P = 32 * 32
-    one = cs["X"][3 * P: 4 * P].clone()
-    alone, _ = run_dx3(cs, "ReLU", check_in=0, X=one, B=1)
-    assert torch.equal(full[3 * P: 4 * P], alone)
+    for i in (3, 129):
+        one = cs["X"][i * P: (i + 1) * P].clone()
+        alone = run_dx3(cs, "ReLU", X=one, B=1)[0]
+        assert torch.equal(full[i * P: (i + 1) * P], alone)
 
 
 def test_dx3_range_guard_sets_flag():
+    """The block input's split (idf_dx3_split_cols) flags NaN and |x| >= 32768."""
     for spike, want in ((40000.0, 1), (float("nan"), 1), (1000.0, 0)):
         cs = make_case(1, 16, 16, 16, 16, True, spike=spike)
-        _, flag = run_dx3(cs, "ReLU")
+        flag = run_dx3(cs, "ReLU")[1]
         assert flag == want, (spike, flag)
 
 
 def test_dx3_output_guard_sets_flag():
     cs = make_case(1, 16, 16, 16, 16, True, scale=4000.0)
-    _, flag = run_dx3(cs, "None", check_in=0)
-    assert flag == 1
+    assert run_dx3(cs, "None")[1] == 1
     cs = make_case(1, 16, 16, 16, 16, True, scale=100.0)
-    _, flag = run_dx3(cs, "None", check_in=0)
-    assert flag == 0
+    assert run_dx3(cs, "None")[1] == 0
 
 
 def test_dx3_unsupported_geometry():

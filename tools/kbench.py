@@ -87,11 +87,17 @@ def main():
             from idfcodec.packing import dx3_weights
             WD, dsc = dx3_weights(np.random.default_rng(0).normal(0, 0.01, (g_alloc, 9, ldw)), c_pad)
             WD = torch.from_numpy(WD.view(np.int16)).to(dev)
+            xs = None
+            if "dx3" in only:
+                nsx = (c_pad + g_pad + 15) // 16
+                xs = torch.empty(nsx * 2 * P * 16, dtype=torch.int16, device=dev)
+                check(lib().idf_dx3_split_cols(s, P, 0, c_pad, ptr(feat), ld, ptr(xs), nsx, ptr(flag)),
+                      "split")
 
             def dx3():
-                check(lib().idf_conv3x3_dx3(s, B, hw, hw, c_pad, ptr(feat), ld, ptr(WD), g_alloc // 16,
+                check(lib().idf_conv3x3_dx3(s, B, hw, hw, c_pad, ptr(xs), nsx, ptr(WD), g_alloc // 16,
                                             dsc, ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
-                                            ptr(feat) + c_pad * 4, ld, 0, 0.0, ptr(flag), 0), "dx3")
+                                            ptr(feat) + c_pad * 4, ld, 0, 0.0, ptr(flag)), "dx3")
 
             from idfcodec.packing import bf16_weights
             WB = torch.from_numpy(bf16_weights(np.random.default_rng(1).normal(
