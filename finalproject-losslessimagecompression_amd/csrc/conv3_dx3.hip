@@ -72,9 +72,71 @@ struct Dx3Args {
 #ifndef IDF_DX3_ABLATE
 #define IDF_DX3_ABLATE 0
 #endif
+// schedule knobs (timing A/Bs; the defaults are the library's): pixel-fragment prefetch
+// distance, a scheduling barrier between steps, the step of the slab's first DMA piece and the
+// steps between pieces
+#ifndef IDF_DX3_DB
+#define IDF_DX3_DB 3
+#endif
+#ifndef IDF_DX3_SB
+#define IDF_DX3_SB 1
+#endif
+#ifndef IDF_DX3_DMA0
+#define IDF_DX3_DMA0 0
+#endif
+#ifndef IDF_DX3_DMAS
+#define IDF_DX3_DMAS 1
+#endif
+// waves 4-7 (the second wave of each SIMD) start their DMA pieces this many steps later
+#ifndef IDF_DX3_STAG
+#define IDF_DX3_STAG 0
+#endif
+// timing-only s_memtime stamps (IDF_DX3_STAMPS=1 builds): per slab, for every wave of the block
+// whose index is IDF_DX3_STAMP_BLOCK -- before the slab's wait, after its barrier, after step 9,
+// at its end; read back with idf_dx3_stamps
+#ifndef IDF_DX3_STAMPS
+#define IDF_DX3_STAMPS 0
+#endif
+#ifndef IDF_DX3_STAMP_BLOCK
+#define IDF_DX3_STAMP_BLOCK 100
+#endif
+#if IDF_DX3_STAMPS
+__device__ unsigned long long g_dx3_stamp[8][40][4];
+#define DX3_STAMP(slab, j)                                                                 \
+  do {                                                                                    \
+    if (blockIdx.x == IDF_DX3_STAMP_BLOCK && (slab) < 40 && lane == 0)                    \
+      g_dx3_stamp[wave][(slab)][(j)] = __builtin_amdgcn_s_memtime();                      \
+  } while (0)
+#else
+#define DX3_STAMP(slab, j) do { } while (0)
+#endif
+// the waves that issue the DMA pieces: IDF_DX3_DMAW of them from wave IDF_DX3_DMAW0
+#ifndef IDF_DX3_DMAW
+#define IDF_DX3_DMAW IDF_DX3_WAVES
+#endif
+#ifndef IDF_DX3_DMAW0
+#define IDF_DX3_DMAW0 0
+#endif
+// 1: cross-slab prefetch -- two barriers per slab: one at its start (the stage slab s - 1 used
+// may be refilled: slab s + 1's DMA is issued), one at step IDF_DX3_X (slab s + 1's stage is
+// complete: the slab's last steps read slab s + 1's first fragments)
+#ifndef IDF_DX3_XPF
+#define IDF_DX3_XPF 0
+#endif
+#ifndef IDF_DX3_X
+#define IDF_DX3_X 20
+#endif
+// 1: one tile per block at every geometry (timing A/B of the two block shapes)
+#ifndef IDF_DX3_FORCE1
+#define IDF_DX3_FORCE1 0
+#endif
 
-constexpr int kDxThreads = 512;
-constexpr int kDxWaves = 8;
+// waves per block (timing A/B: 16 = four per SIMD at 2 rows per wave)
+#ifndef IDF_DX3_WAVES
+#define IDF_DX3_WAVES 8
+#endif
+constexpr int kDxWaves = IDF_DX3_WAVES;
+constexpr int kDxThreads = 64 * kDxWaves;
 constexpr int kDxCW = 18;                 // halo canvas width (slots) = tile width 16 + 2
 constexpr int kDxSlots = kDxCW * kDxCW;   // 324
 constexpr int kDxPlane = 11 * 1024;       // one plane (xh or xl): 324 x 32 B in whole 1-KiB pieces
@@ -87,7 +149,7 @@ constexpr float kDxOutGuard = 8192.0f;
 
 template <int NF, int WR>
 struct Dx3Lds {
-  static constexpr int T = WR / 2;                 // 16x16 tiles per block
+  static constexpr int T = WR * kDxWaves / 16;     // 16x16 tiles per block
   static constexpr int HR = WR + 2;                // halo rows a wave reads
   static constexpr int NS = 5 * HR - 1;            // steps per slab (see the schedule)
   static constexpr int WOFF = T * 2 * kDxPlane;    // weights within a stage
@@ -99,7 +161,7 @@ struct Dx3Lds {
   static constexpr int BYTES = BOFF + 16 * NF * 16 * 4;
   static constexpr int HPIECES = T * 2 * kDxPlanePieces;   // halo DMA pieces per slab
   static constexpr int NPIECES = HPIECES + WST / 1024;     // + weight pieces
-  static constexpr int PPW = (NPIECES + kDxWaves - 1) / kDxWaves;  // pieces per wave (max)
+  static constexpr int PPW = (NPIECES + IDF_DX3_DMAW - 1) / IDF_DX3_DMAW;  // pieces per wave (max)
 };
 
 typedef __attribute__((address_space(3))) void* dx_lds_ptr_t;
@@ -140,7 +202,8 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   uint32_t pbase[L::PPW];  // per piece: source byte offset of slab 0 (halo) / within a slab (weights)
 #pragma unroll
   for (int i = 0; i < L::PPW; ++i) {
-    const int k = wave + kDxWaves * i;
+    const int dw = wave - IDF_DX3_DMAW0;  // this wave's rank among the DMA-issuing waves
+    const int k = (dw >= 0 && dw < IDF_DX3_DMAW) ? dw + IDF_DX3_DMAW * i : (1 << 20);
     pbase[i] = kDxInvalid;
     if (k < L::HPIECES) {
       const int t = k / (2 * kDxPlanePieces), pl = (k / kDxPlanePieces) % 2, pi = k % kDxPlanePieces;
@@ -163,7 +226,8 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   }
   // issue piece i of slab s into stage st
   auto dma = [&](int s, int st, int i) {
-    const int k = wave + kDxWaves * i;
+    const int dw = wave - IDF_DX3_DMAW0;
+    const int k = (dw >= 0 && dw < IDF_DX3_DMAW) ? dw + IDF_DX3_DMAW * i : (1 << 20);
     if (k >= L::NPIECES) return;
     // one call site for both kinds of piece (the LDS address formed from the __shared__ array
     // itself): the host pass of hipcc drops the kernel's launch stub otherwise
@@ -235,10 +299,10 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   //   steps [4 HR, NS)    (G, h = t - 4 HR):            [wl(0,2) ; wl(1,2)] and [0 ; wl(2,2)]
   //                                                      . [xh(h,2) | xh(h+1,2)]
   // Pixel fragments are read DB steps ahead (a ring of DB + 1), a phase's weight fragments in
-  // the three steps before it.  Two LDS stages: slab s reads stage s % 2; after the slab's
+  // the first three steps of the phase before it.  Two LDS stages: slab s reads stage s % 2; after the slab's
   // barrier (every wave's DMA of slab s landed, every wave done with slab s - 1) the waves DMA
   // slab s + 1 into the other stage, one piece per step.
-  constexpr int DB = 3, RB = DB + 1;
+  constexpr int DB = IDF_DX3_DB, RB = DB + 1;
   e8 Bq[RB];
   e8 AS[2][3][NF];  // weight sets: P0 / P2 in 0, P1 / F in 1
   e8 AZ[2][NF];     // G: [wl(0,2) ; wl(1,2)] and [0 ; wl(2,2)]
@@ -265,60 +329,159 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   };
 
   const int nslab = g.nslab;
-  if (nslab > 0) {
+  if constexpr (IDF_DX3_XPF) {
+    constexpr int X = (IDF_DX3_X < NS - DB && IDF_DX3_X + 1 >= 3 * HR) ? IDF_DX3_X : NS - DB - 3;
+    static_assert(X + 1 >= 3 * HR && NS - DB > X && X >= L::PPW, "cross-slab prefetch schedule");
+    if (nslab > 0) {
 #pragma unroll
-    for (int i = 0; i < L::PPW; ++i) dma(0, 0, i);
-  }
-  for (int s = 0; s < nslab; ++s) {
-    const char* cur = lds + (s & 1) * L::STAGE;
-    // this wave's DMA of slab s landed; after the barrier every wave's has, and every wave is
-    // done reading stage (s + 1) % 2 (slab s - 1)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!(IDF_DX3_ABLATE & 8)) __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
+      for (int i = 0; i < L::PPW; ++i) dma(0, 0, i);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (nslab > 1) {
 #pragma unroll
-    for (int dy = 0; dy < 3; ++dy) read_A(cur, 0, dy, AS[0][dy]);
-#pragma unroll
-    for (int k = 0; k < DB; ++k) Bq[k] = read_B(cur, k);
-    const bool more = s + 1 < nslab;
-    auto step = [&](auto tc) {
-      constexpr int t = decltype(tc)::value;
-      __builtin_amdgcn_sched_barrier(0);  // keep the schedule: steps do not mix
-      // slab s + 1's DMA, one piece per step
-      if constexpr (t < L::PPW) {
-        if (more) dma(s + 1, (s + 1) & 1, t);
+        for (int i = 0; i < L::PPW; ++i) dma(1, 1, i);
       }
-      // weights of the next phase, one kernel row per step
-      if constexpr (t >= HR - 3 && t < HR) read_A(cur, 1, t - (HR - 3), AS[1][t - (HR - 3)]);
-      if constexpr (t >= 2 * HR - 3 && t < 2 * HR) read_A(cur, 2, t - (2 * HR - 3), AS[0][t - (2 * HR - 3)]);
-      if constexpr (t >= 3 * HR - 3 && t < 3 * HR) read_A(cur, 3, t - (3 * HR - 3), AS[1][t - (3 * HR - 3)]);
-      if constexpr (t == 4 * HR - 3 || t == 4 * HR - 2) {
 #pragma unroll
-        for (int n = 0; n < NF; ++n) {
-          if (t == 4 * HR - 3) AZ[0][n] = rdA(cur + oAG + n * 512);
-          else AZ[1][n] = rdA(zlane ? zO + n * 512 : cur + oAO + n * 512);
-        }
-      }
-      // pixel fragment DB steps ahead (within the slab)
-      if constexpr (t + DB < NS) Bq[(t + DB) % RB] = read_B(cur, t + DB);
-      const e8& Bv = Bq[t % RB];
-      if constexpr (t < 3 * HR) {
-        mma_rows(AS[(t / HR) & 1], Bv, t % HR);
-      } else if constexpr (t < 4 * HR) {
-        mma_rows(AS[1], Bv, t - 3 * HR);
-      } else {
-        constexpr int h = t - 4 * HR;
-        if constexpr (h < WR) {
+      for (int dy = 0; dy < 3; ++dy) read_A(lds, 0, dy, AS[0][dy]);
 #pragma unroll
-          for (int n = 0; n < NF; ++n) mma(AZ[0][n], Bv, acc[h][n]);
+      for (int k = 0; k < DB; ++k) Bq[k] = read_B(lds, k);
+    }
+    for (int s = 0; s < nslab; ++s) {
+      const char* cur = lds + (s & 1) * L::STAGE;
+      const char* nxt = lds + ((s + 1) & 1) * L::STAGE;
+      const bool more = s + 1 < nslab;
+      DX3_STAMP(s, 0);
+      // every wave is done with slab s - 1: its stage may take slab s + 1
+      if (s >= 1) __builtin_amdgcn_s_barrier();
+      DX3_STAMP(s, 1);
+      auto step = [&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        if (IDF_DX3_SB) __builtin_amdgcn_sched_barrier(0);
+        if constexpr (t == 9) DX3_STAMP(s, 2);
+        if constexpr (t < L::PPW) {
+          if (s >= 1 && more) dma(s + 1, (s + 1) & 1, t);
         }
-        if constexpr (h > 0) {
+        if constexpr (t == X) {  // slab s + 1's stage complete (every wave's DMA landed)
+          if (more) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+          }
+        }
+        if constexpr (t < 3) read_A(cur, 1, t, AS[1][t]);
+        if constexpr (t >= HR && t < HR + 3) read_A(cur, 2, t - HR, AS[0][t - HR]);
+        if constexpr (t >= 2 * HR && t < 2 * HR + 3) read_A(cur, 3, t - 2 * HR, AS[1][t - 2 * HR]);
+        if constexpr (t == 2 * HR + 3 || t == 2 * HR + 4) {
 #pragma unroll
-          for (int n = 0; n < NF; ++n) mma(AZ[1][n], Bv, acc[h - 1][n]);
+          for (int n = 0; n < NF; ++n) {
+            if (t == 2 * HR + 3) AZ[0][n] = rdA(cur + oAG + n * 512);
+            else AZ[1][n] = rdA(zlane ? zO + n * 512 : cur + oAO + n * 512);
+          }
         }
-      }
-    };
-    dx_unroll(step, std::make_integer_sequence<int, NS>{});
+        // slab s + 1's first weights (AS[0] is free once phase 2 is done)
+        if constexpr (t > X && t <= X + 3) {
+          if (more) read_A(nxt, 0, t - X - 1, AS[0][t - X - 1]);
+        }
+        if constexpr (t + DB < NS) Bq[(t + DB) % RB] = read_B(cur, t + DB);
+        else if (more) Bq[(t + DB) % RB] = read_B(nxt, t + DB - NS);
+        const e8& Bv = Bq[t % RB];
+        if constexpr (t < 3 * HR) {
+          mma_rows(AS[(t / HR) & 1], Bv, t % HR);
+        } else if constexpr (t < 4 * HR) {
+          mma_rows(AS[1], Bv, t - 3 * HR);
+        } else {
+          constexpr int h = t - 4 * HR;
+          if constexpr (h < WR) {
+#pragma unroll
+            for (int n = 0; n < NF; ++n) mma(AZ[0][n], Bv, acc[h][n]);
+          }
+          if constexpr (h > 0) {
+#pragma unroll
+            for (int n = 0; n < NF; ++n) mma(AZ[1][n], Bv, acc[h - 1][n]);
+          }
+        }
+      };
+      dx_unroll(step, std::make_integer_sequence<int, NS>{});
+      DX3_STAMP(s, 3);
+      // the ring ran NS steps: slab s + 1's fragment k is in Bq[(NS + k) % RB]
+      e8 f[DB];
+#pragma unroll
+      for (int k = 0; k < DB; ++k) f[k] = Bq[(NS + k) % RB];
+#pragma unroll
+      for (int k = 0; k < DB; ++k) Bq[k] = f[k];
+    }
+  } else {
+    const int nslab = g.nslab;
+    if (nslab > 0) {
+#pragma unroll
+      for (int i = 0; i < L::PPW; ++i) dma(0, 0, i);
+    }
+    for (int s = 0; s < nslab; ++s) {
+      const char* cur = lds + (s & 1) * L::STAGE;
+      // this wave's DMA of slab s landed; after the barrier every wave's has, and every wave is
+      // done reading stage (s + 1) % 2 (slab s - 1)
+      DX3_STAMP(s, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (!(IDF_DX3_ABLATE & 8)) __builtin_amdgcn_s_barrier();
+      DX3_STAMP(s, 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) read_A(cur, 0, dy, AS[0][dy]);
+#pragma unroll
+      for (int k = 0; k < DB; ++k) Bq[k] = read_B(cur, k);
+      const bool more = s + 1 < nslab;
+      auto step = [&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        if (IDF_DX3_SB) __builtin_amdgcn_sched_barrier(0);  // keep the schedule: steps do not mix
+        if constexpr (t == 9) DX3_STAMP(s, 2);
+        // slab s + 1's DMA, one piece every IDF_DX3_DMAS steps from step IDF_DX3_DMA0
+        constexpr int ds = IDF_DX3_DMAS > 0 ? IDF_DX3_DMAS : 1;
+        auto dma_at = [&](auto dtc) {
+          constexpr int dt = decltype(dtc)::value;
+          if constexpr (IDF_DX3_DMAS == 0 && dt == 0) {  // the whole slab's pieces at once
+            if (more) {
+#pragma unroll
+              for (int i = 0; i < L::PPW; ++i) dma(s + 1, (s + 1) & 1, i);
+            }
+          } else if constexpr (IDF_DX3_DMAS > 0 && dt >= 0 && dt % ds == 0 && dt / ds < L::PPW) {
+            if (more) dma(s + 1, (s + 1) & 1, dt / ds);
+          }
+        };
+        if (IDF_DX3_STAG == 0 || !(wave & 4)) dma_at(std::integral_constant<int, t - IDF_DX3_DMA0>{});
+        else dma_at(std::integral_constant<int, t - IDF_DX3_DMA0 - IDF_DX3_STAG>{});
+        // weights of the next phase, one kernel row per step, in the first three steps of the
+        // phase before it (its register set was freed by the phase before that)
+        if constexpr (t < 3) read_A(cur, 1, t, AS[1][t]);
+        if constexpr (t >= HR && t < HR + 3) read_A(cur, 2, t - HR, AS[0][t - HR]);
+        if constexpr (t >= 2 * HR && t < 2 * HR + 3) read_A(cur, 3, t - 2 * HR, AS[1][t - 2 * HR]);
+        if constexpr (t == 2 * HR + 3 || t == 2 * HR + 4) {
+#pragma unroll
+          for (int n = 0; n < NF; ++n) {
+            if (t == 2 * HR + 3) AZ[0][n] = rdA(cur + oAG + n * 512);
+            else AZ[1][n] = rdA(zlane ? zO + n * 512 : cur + oAO + n * 512);
+          }
+        }
+        // pixel fragment DB steps ahead (within the slab)
+        if constexpr (t + DB < NS) Bq[(t + DB) % RB] = read_B(cur, t + DB);
+        const e8& Bv = Bq[t % RB];
+        if constexpr (t < 3 * HR) {
+          mma_rows(AS[(t / HR) & 1], Bv, t % HR);
+        } else if constexpr (t < 4 * HR) {
+          mma_rows(AS[1], Bv, t - 3 * HR);
+        } else {
+          constexpr int h = t - 4 * HR;
+          if constexpr (h < WR) {
+#pragma unroll
+            for (int n = 0; n < NF; ++n) mma(AZ[0][n], Bv, acc[h][n]);
+          }
+          if constexpr (h > 0) {
+#pragma unroll
+            for (int n = 0; n < NF; ++n) mma(AZ[1][n], Bv, acc[h - 1][n]);
+          }
+        }
+      };
+      dx_unroll(step, std::make_integer_sequence<int, NS>{});
+      DX3_STAMP(s, 3);
+    }
   }
 
   // ---- epilogue: lane holds outputs 16n + 4q .. +3 of pixel (row r0 + m, column j) of its
@@ -398,13 +561,21 @@ __global__ void __launch_bounds__(256) dx3_split_cols_kernel(int64_t P, int32_t 
   char* p = (char*)xs + ((int64_t)(c >> 4) * 2 * P + pix) * 32 + (c & 15) * 2;
   *(e4*)p = h;
   *(e4*)(p + P * 32) = l;
-  const float m = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
-  if (!(m < kDxInGuard) && flag) atomicOr(flag, 1u);
+  // each value compared on its own: fmaxf would drop a NaN
+  const bool ok = fabsf(v[0]) < kDxInGuard && fabsf(v[1]) < kDxInGuard &&
+                  fabsf(v[2]) < kDxInGuard && fabsf(v[3]) < kDxInGuard;
+  if (!ok && flag) atomicOr(flag, 1u);
 }
 
 }  // namespace idf
 
 using namespace idf;
+
+#if IDF_DX3_STAMPS
+extern "C" int idf_dx3_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dx3_stamp), sizeof(g_dx3_stamp)) == hipSuccess ? 0 : 2;
+}
+#endif
 
 extern "C" int idf_conv3x3_dx3_supported(int32_t H, int32_t W, int32_t N) {
   return H >= 1 && W >= 16 && W % 16 == 0 && N >= 1 && N <= 48;
@@ -456,14 +627,15 @@ extern "C" int idf_conv3x3_dx3(void* stream, int32_t B, int32_t H, int32_t W, in
   hipStream_t s = (hipStream_t)stream;
   // two tiles per block (4 rows per wave) while that still gives every CU a block; else one
   // tile per block (2 rows per wave)
-  const bool two = ntiles >= 2 * 256;
+  const bool two = ntiles >= 2 * 256 && !IDF_DX3_FORCE1;
 #define IDF_DX3_LAUNCH(nf_, wr_)                                                                   \
-  hipLaunchKernelGGL((conv3_dx3_kernel<nf_, wr_>), dim3((unsigned)((ntiles + wr_ / 2 - 1) / (wr_ / 2))), \
+  hipLaunchKernelGGL((conv3_dx3_kernel<nf_, wr_>),                                               \
+                     dim3((unsigned)((ntiles + Dx3Lds<nf_, wr_>::T - 1) / Dx3Lds<nf_, wr_>::T)), \
                      dim3(kDxThreads), 0, s, g)
   switch (nf) {
-    case 1: if (two) IDF_DX3_LAUNCH(1, 4); else IDF_DX3_LAUNCH(1, 2); break;
-    case 2: if (two) IDF_DX3_LAUNCH(2, 4); else IDF_DX3_LAUNCH(2, 2); break;
-    default: if (two) IDF_DX3_LAUNCH(3, 4); else IDF_DX3_LAUNCH(3, 2); break;
+    case 1: if (two) IDF_DX3_LAUNCH(1, 32 / kDxWaves); else IDF_DX3_LAUNCH(1, 16 / kDxWaves); break;
+    case 2: if (two) IDF_DX3_LAUNCH(2, 32 / kDxWaves); else IDF_DX3_LAUNCH(2, 16 / kDxWaves); break;
+    default: if (two) IDF_DX3_LAUNCH(3, 32 / kDxWaves); else IDF_DX3_LAUNCH(3, 16 / kDxWaves); break;
   }
 #undef IDF_DX3_LAUNCH
   return idf_last_error();
