@@ -43,10 +43,10 @@ WINO = os.environ.get("IDF_WINO", "1") != "0"
 # range guard that falls back to the exact-f32 kernel; IDF_WX3=0 always uses the latter.
 WX3 = os.environ.get("IDF_WX3", "1") != "0"
 # ... and, where the geometry allows (images a multiple of 16 wide: conv3_dx3.hip), as the direct
-# conv on the same split-f16 products with no transform ("dx3"), opt-in with IDF_DX3=1 while it
-# measures slower than wx3 at the wide layers.  Conv modes: 'dx3' (dx3 where supported, wx3
-# elsewhere), 'x3', 'f32'; the mode is recorded in the bitstream.
-DX3 = os.environ.get("IDF_DX3", "0") == "1"
+# conv on the same split-f16 products with no transform ("dx3", the default mode: bench +1.4%
+# same-box, encode -0.8 ms); IDF_DX3=0 keeps every layer on wx3.  Conv modes: 'dx3' (dx3 where
+# supported, wx3 elsewhere), 'x3', 'f32'; the mode is recorded in the bitstream.
+DX3 = os.environ.get("IDF_DX3", "1") != "0"
 
 
 class DeviceBlock:
