@@ -33,6 +33,10 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(REPO, "finalproject-losslessimagecompression_amd")
 sys.path.insert(0, PKG)
+# hardware queues per process: the pipelined steps use six HIP streams (the encode's and its
+# rANS side stream, the decode's and its two lanes, the default); with HIP's default of 4 two
+# of them would share a queue and run in order.  Set before anything initialises HIP.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -57,6 +61,11 @@ def parse():
                     help="PROCSxTHREADS for the CPU-baseline pool (default: one thread per "
                          "usable CPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="1: step k's decode runs beside step k+1's encode (two HIP streams, "
+                         "separate engine workspaces; every timed step still encodes and "
+                         "decodes one whole batch, pipeline fill and drain inside the timed "
+                         "region); 0: each step's encode and decode back to back")
     ap.add_argument("--no-residual", action="store_true",
                     help="skip the residual configs 3-5 extras")
     ap.add_argument("--launch-probe", action="store_true",
@@ -564,8 +573,61 @@ def main():
         e2.record()
         return bs, full, out, (e0, e1, e2)
 
-    for _ in range(args.warmup):
-        step()
+    # Pipelined steps: the encode of batch k+1 (stream E, engine workspace ENC_SLOT) runs
+    # beside the decode of batch k (stream D, the decode lanes' workspaces): the decode's
+    # serial rANS chains, which its own lanes cannot hide, overlap the next encode's convs.
+    # Each batch's decode waits on an event recorded after its encode (and, N > 1, after its
+    # gather -> scatter); the bitstreams stay referenced until the loop ends.
+    enc_stream = dec_stream = None
+    if args.pipeline:
+        enc_stream, dec_stream = _lib.new_stream(dev), _lib.new_stream(dev)
+
+    def encode_part():
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(enc_stream):
+            a.record()
+            bs = codec.encode(img, slot=codec.ENC_SLOT)
+            full = None
+            if world > 1:
+                full = gather_bitstream(bs, dst=0)
+                bs, _ = scatter_bitstream(full, src=0, device=dev)
+            b.record()
+        return bs, full, (a, b)
+
+    def decode_part(bs, after):
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(dec_stream):
+            dec_stream.wait_event(after)
+            a.record()
+            out, _ = codec.decode(bs, verify=False)
+            b.record()
+        return out, (a, b)
+
+    def run_steps(n):
+        res = [step() for _ in range(n)]
+        return res[-1][0], res[-1][1], res[-1][2], [((e0, e1), (e1, e2)) for *_, (e0, e1, e2) in res]
+
+    def run_steps_pipelined(n):
+        keep, evs = [], []
+        bs, full, ee = encode_part()
+        keep.append((bs, full, ee))
+        out = None
+        for k in range(n):
+            prev_bs, prev_full, prev_ee = keep[-1]
+            out, de = decode_part(prev_bs, prev_ee[1])  # batch k's decode ...
+            evs.append((prev_ee, de))
+            if k + 1 < n:
+                keep.append(encode_part())  # ... beside batch k+1's encode
+        last_bs, last_full, _ = keep[-1]
+        return last_bs, last_full, out, evs
+
+    if args.pipeline:
+        run_steps = run_steps_pipelined  # noqa: F811
+
+    if args.warmup:
+        run_steps(args.warmup)
     if pool is not None:
         pool.wait_ready()  # the workers' start-up never overlaps the timed steps
     torch.cuda.synchronize()
@@ -574,10 +636,7 @@ def main():
     torch.cuda.synchronize()
     codec.coder.trace = []  # HIP events around the rANS launches of the timed steps
     t0 = time.perf_counter()
-    evs = []
-    for _ in range(args.steps):
-        bs, full, out, ev = step()
-        evs.append(ev)
+    bs, full, out, evs = run_steps(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -589,8 +648,21 @@ def main():
     elapsed = float(t.item())
     rans = rans_roofline(codec.coder.trace, bs, args.steps)
     codec.coder.trace = None
-    enc_ms = sum(a.elapsed_time(b) for a, b, _ in evs) / len(evs)
-    dec_ms = sum(b.elapsed_time(c) for _, b, c in evs) / len(evs)
+    # per batch: the encode's and the decode's own stream time (pipelined: while overlapping)
+    enc_ms = sum(e[0].elapsed_time(e[1]) for e, _ in evs) / len(evs)
+    dec_ms = sum(d[0].elapsed_time(d[1]) for _, d in evs) / len(evs)
+    serial = None
+    if args.pipeline:
+        # the same steps back to back (untimed for `value`): what one batch costs alone
+        pe = []
+        for _ in range(2):
+            pe.append(step())
+        torch.cuda.synchronize()
+        se = sum(a.elapsed_time(b) for *_, (a, b, c) in pe) / len(pe)
+        sd = sum(b.elapsed_time(c) for *_, (a, b, c) in pe) / len(pe)
+        serial = {"encode_ms": round(se, 3), "decode_ms": round(sd, 3),
+                  "ms_per_step": round(se + sd, 3),
+                  "mpx_s": round(world * B * PX_PER_IMG / (se + sd) / 1e3, 4)}
 
     # exactness of the last timed step on every rank (and, N > 1, of the whole gathered
     # single-batch bitstream decoded on rank 0 alone, below)
@@ -673,6 +745,13 @@ def main():
             "decode_mpx_s": round(B * PX_PER_IMG / dec_ms / 1e3, 4),
             "encode_ms": round(enc_ms, 3),
             "decode_ms": round(dec_ms, 3),
+            "pipelined": bool(args.pipeline),
+            "step_overlap": ("step k's decode runs beside step k+1's encode on a second HIP "
+                             "stream (encode_ms / decode_ms: each part's own stream time while "
+                             "overlapping); every timed step encodes and decodes one whole "
+                             "batch, pipeline fill and drain inside the timed region"
+                             if args.pipeline else None),
+            "serial": serial,
             "bpp": round(bpp, 4),
             "bits_per_subpixel": round(bpp / 3, 4),
             "round_trip_exact": exact,

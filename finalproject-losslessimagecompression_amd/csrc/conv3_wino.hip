@@ -956,10 +956,22 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   float* pbase = g.part ? g.part + ((int64_t)ks * ((int64_t)g.B * g.H * g.Wd) + pix0) * g.ldp : nullptr;
   const float* rbase = g.res ? g.res + pix0 * g.ldr : nullptr;
   const bool vec = REGS && g.ksplit == 1 && !g.res && g.vec4;
+  // Scalar epilogue: thread (it) finishes tile e_t(it) at output channel e_nn.  With REGS
+  // staging the 16 lanes of each ds_read_b128 lane group ({0-3,12-15,20-27}, {4-11,16-19,28-31}
+  // and the same + 32) take one tile and the 16 channels, so a group's reads (rows 1284 floats
+  // apart, 4 banks each) hit all 64 banks once: the plain lane >> 4 / lane & 15 split gave the
+  // 8x8 level's epilogue 2-way conflicts (47% of its LDS cycles, profiles/r03/pmc_x3).
+  int e_grp = tid >> 4 & 3, e_nn = tid & 15;
+  if constexpr (REGS) {
+    const int m = lane & 31;
+    const bool g0 = m < 4 || (m >= 12 && m < 16) || (m >= 20 && m < 28);
+    e_grp = 2 * (lane >> 5) + (g0 ? 0 : 1);
+    e_nn = m < 4 ? m : m < 12 ? m - 4 : m < 16 ? m - 8 : m < 20 ? m - 8 : m < 28 ? m - 12 : m - 16;
+  }
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     if (vec) break;  // the vector epilogue computes its own pixel map below
-    const int t = (tid + kWThreads * it) >> 4;
+    const int t = 4 * wave + 32 * it + e_grp;  // = (tid + kWThreads * it) >> 4 without REGS
     const int img = udiv_s(t, TPI);
     const int rem = t - img * TPI;
     const int ty = udiv_s(rem, TTW), tx = rem - ty * TTW;
@@ -1148,7 +1160,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
     if (IDF_WINO_STAMPS) st_e[1 + 2 * j] = __builtin_amdgcn_s_memtime();
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
-      const int t = (tid + kWThreads * it) >> 4, nn = tid & 15;
+      const int t = 4 * wave + 32 * it + e_grp, nn = e_nn;
       const int n = (nf0 + j) * 16 + nn;
       if (e_img[it] < g.IMGS && n < g.N) {
         float m[4][4];

@@ -382,15 +382,22 @@ class ImageCodec:
         self._streams = []
         self.lane_marks = None
 
+    # engine workspace slot of an encode that may run beside a decode (encode_decode_stream):
+    # the decode lanes hold slots 0 .. lanes - 1
+    ENC_SLOT = 8
+
     @torch.no_grad()
-    def encode(self, img_u8: torch.Tensor, cond=None, compact: bool = True) -> Bitstream:
+    def encode(self, img_u8: torch.Tensor, cond=None, compact: bool = True,
+               slot: int = 0) -> Bitstream:
+        """slot: the engine workspace set the flow runs in (a different one from the decode
+        lanes' lets an encode overlap a decode on another stream, encode_decode_stream)."""
         _lib.require_device(img_u8, "image batch")
         if img_u8.dtype != torch.uint8:
             raise TypeError("ImageCodec.encode expects uint8 images")
         B = img_u8.shape[0]
         img_u8 = img_u8.contiguous()
-        return self._encode_guarded(lambda: self.engine.load_u8(img_u8), B, cond, compact,
-                                    lanes_img=img_u8)
+        return self._encode_guarded(lambda: self.engine.load_u8(img_u8, slot), B, cond, compact,
+                                    lanes_img=img_u8 if slot == 0 else None, slot=slot)
 
     def _encode_lanes(self, img_u8, B: int, nl: int, compact: bool) -> Bitstream:
         """Encode lanes (IDF_ENC_LANES): the batch's flow as nl equal sub-batches on the
@@ -446,7 +453,7 @@ class ImageCodec:
             main.wait_stream(st)
         return enc.finish(compact=compact)
 
-    def _encode_guarded(self, load, B, cond, compact, lanes_img=None):
+    def _encode_guarded(self, load, B, cond, compact, lanes_img=None, slot: int = 0):
         """Encode in the engine's conv mode; if the split-f16 range guard tripped (a value
         beyond its f16 range), recompute the batch with the exact-f32 convs.  The mode that
         produced the streams is recorded in the bitstream (meta['conv'], container flag)."""
@@ -476,20 +483,20 @@ class ImageCodec:
         elif enc is not None:
             load()
             try:
-                eng.forward_pm(B, cond=cond, on_level=enc.level)
+                eng.forward_pm(B, cond=cond, slot=slot, on_level=enc.level)
             finally:
                 # never free or reuse main-stream buffers while side launches may run
                 enc.join()
             bs = enc.finish(compact=compact)
         else:
             ws = load()
-            eng.forward_pm(B, cond=cond)
+            eng.forward_pm(B, cond=cond, slot=slot)
             bs = self.coder.encode(ws, B, compact=compact)
         if mode in ("x3", "dx3") and eng.range_flag_tripped():
             eng.set_conv_mode("f32")
             try:
                 ws = load()
-                eng.forward_pm(B, cond=cond)
+                eng.forward_pm(B, cond=cond, slot=slot)
                 bs = self.coder.encode(ws, B, compact=compact)
             finally:
                 eng.set_conv_mode(mode)
