@@ -61,7 +61,7 @@ def parse():
                     help="PROCSxTHREADS for the CPU-baseline pool (default: one thread per "
                          "usable CPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pipeline", type=int, default=0,
+    ap.add_argument("--pipeline", type=int, default=1,
                     help="1: step k's decode runs beside step k+1's encode (two HIP streams, "
                          "separate engine workspaces; every timed step still encodes and "
                          "decodes one whole batch, pipeline fill and drain inside the timed "

@@ -102,6 +102,13 @@ struct Dx3Args {
 #endif
 #if IDF_DX3_STAMPS
 __device__ unsigned long long g_dx3_stamp[8][40][4];
+// per wave: kernel entry, after the bias table, loop end, kernel end (s_memtime), and
+// s_memrealtime (100 MHz) at entry and end -- the clock the loop ran at
+__device__ unsigned long long g_dx3_phase[8][6];
+#define DX3_PHASE(j, v)                                                                      \
+  do {                                                                                      \
+    if (blockIdx.x == IDF_DX3_STAMP_BLOCK && lane == 0) g_dx3_phase[wave][(j)] = (v);       \
+  } while (0)
 #define DX3_STAMP(slab, j)                                                                 \
   do {                                                                                    \
     if (blockIdx.x == IDF_DX3_STAMP_BLOCK && (slab) < 40 && lane == 0)                    \
@@ -109,6 +116,7 @@ __device__ unsigned long long g_dx3_stamp[8][40][4];
   } while (0)
 #else
 #define DX3_STAMP(slab, j) do { } while (0)
+#define DX3_PHASE(j, v) do { } while (0)
 #endif
 // the waves that issue the DMA pieces: IDF_DX3_DMAW of them from wave IDF_DX3_DMAW0
 #ifndef IDF_DX3_DMAW
@@ -248,8 +256,16 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   };
 
   // zeros for the odd tap's pair, and the epilogue's bias table (both outside the stages)
+  // slab 0's DMA first: the bias table's dependent global loads below then overlap its latency
+  if (g.nslab > 0) {
+#pragma unroll
+    for (int i = 0; i < L::PPW; ++i) dma(0, 0, i);
+  }
   for (int e = tid; e < NF * 512 / 16; e += kDxThreads) *(d4*)(lds + L::ZOFF + 16 * e) = d4{0.f, 0.f, 0.f, 0.f};
+  DX3_PHASE(0, __builtin_amdgcn_s_memtime());
+  DX3_PHASE(4, __builtin_amdgcn_s_memrealtime());
   stage_bias((float*)(lds + L::BOFF), NF * 16, 0, g.N, g.b3, g.vtap, g.bfull, g.ldv, tid, kDxThreads);
+  DX3_PHASE(1, __builtin_amdgcn_s_memtime());
 
   // ---- fragment read offsets (bytes from a stage base).  B (pixels): lane (q = lane >> 4,
   // j = lane & 15) reads pixel j of a halo row, 8 channels.  A (weights): output j, 8 channels.
@@ -333,8 +349,6 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
     constexpr int X = (IDF_DX3_X < NS - DB && IDF_DX3_X + 1 >= 3 * HR) ? IDF_DX3_X : NS - DB - 3;
     static_assert(X + 1 >= 3 * HR && NS - DB > X && X >= L::PPW, "cross-slab prefetch schedule");
     if (nslab > 0) {
-#pragma unroll
-      for (int i = 0; i < L::PPW; ++i) dma(0, 0, i);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       if (nslab > 1) {
@@ -411,10 +425,6 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
     }
   } else {
     const int nslab = g.nslab;
-    if (nslab > 0) {
-#pragma unroll
-      for (int i = 0; i < L::PPW; ++i) dma(0, 0, i);
-    }
     for (int s = 0; s < nslab; ++s) {
       const char* cur = lds + (s & 1) * L::STAGE;
       // this wave's DMA of slab s landed; after the barrier every wave's has, and every wave is
@@ -488,6 +498,7 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   // tile.  fp32 outputs to out; their split pairs to XS at channel C + 16n + 4q (zeros for the
   // padding outputs n >= N and on to the next 16-channel boundary past C + N, so the next
   // layer's last slab reads finite values; never past the split buffer).
+  DX3_PHASE(2, __builtin_amdgcn_s_memtime());
   if (tile >= g.ntiles) return;
   int qt = tile;
   const int tx = qt - udiv_s(qt, g.tiles_x) * g.tiles_x;
@@ -539,6 +550,8 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
     }
   }
   if (!out_ok && g.flag) atomicOr(g.flag, 1u);
+  DX3_PHASE(3, __builtin_amdgcn_s_memtime());
+  DX3_PHASE(5, __builtin_amdgcn_s_memrealtime());
 }
 
 // Block-input split: XS channels [c0, c1) of every pixel from the fp32 rows x (ld_x floats),
@@ -573,7 +586,8 @@ using namespace idf;
 
 #if IDF_DX3_STAMPS
 extern "C" int idf_dx3_stamps(unsigned long long* host) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dx3_stamp), sizeof(g_dx3_stamp)) == hipSuccess ? 0 : 2;
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dx3_stamp), sizeof(g_dx3_stamp)) != hipSuccess) return 2;
+  return hipMemcpyFromSymbol(host + 8 * 40 * 4, HIP_SYMBOL(g_dx3_phase), sizeof(g_dx3_phase)) == hipSuccess ? 0 : 2;
 }
 #endif
 

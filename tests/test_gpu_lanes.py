@@ -135,3 +135,31 @@ def test_encode_lanes_identical(B, lanes):
     assert n > 0
     out, info = codec.decode(got)
     assert info["ok"] and torch.equal(out, img)
+
+
+def test_encode_beside_decode_exact():
+    """bench.py --pipeline 1: batch A's decode (its own stream, the lanes' workspaces) runs
+    while batch B is encoded on another stream in workspace slot ENC_SLOT.  A decodes exactly,
+    and B's bitstream is bit-identical to B encoded alone."""
+    from idfcodec import _lib, configs, synthetic
+    model = synthetic.build_model(configs.get("imagenet64")).cuda()
+    codec = model.codec()
+    a = synthetic.images(32, seed=71).cuda()
+    b = synthetic.images(32, seed=72).cuda()
+    bs_a = codec.encode(a)
+    ref_b = codec.encode(b)
+    torch.cuda.synchronize()
+    E, D = _lib.new_stream(), _lib.new_stream()
+    done_a = torch.cuda.Event()
+    done_a.record()
+    for _ in range(2):  # the second time with every cache warm
+        with torch.cuda.stream(D):
+            D.wait_event(done_a)
+            out_a, info_a = codec.decode(bs_a, verify=False)
+        with torch.cuda.stream(E):
+            bs_b = codec.encode(b, slot=codec.ENC_SLOT)
+        torch.cuda.synchronize()
+        assert torch.equal(out_a, a)
+        assert bool((info_a["final_states"] == 1 << 32).all())
+        assert torch.equal(bs_b.states, ref_b.states) and torch.equal(bs_b.nwords, ref_b.nwords)
+        assert torch.equal(bs_b.words, ref_b.words) and bs_b.meta["conv"] == ref_b.meta["conv"]

@@ -17,7 +17,7 @@ import kbench  # noqa: E402
 from idfcodec._lib import lib  # noqa: E402
 
 kbench.main()
-buf = (ctypes.c_ulonglong * (8 * 40 * 4))()
+buf = (ctypes.c_ulonglong * (8 * 40 * 4 + 8 * 6))()
 assert lib().idf_dx3_stamps(buf) == 0
 for w in range(8):
     rows = [[buf[(w * 40 + s) * 4 + j] for j in range(4)] for s in range(31)]
@@ -28,3 +28,9 @@ for w in range(8):
     m = lambda v: sum(v) / len(v)  # noqa: E731
     print(f"wave {w}: wait {m(wait):7.0f}  steps0-8 {m(a):7.0f}  steps9-end {m(b):7.0f}  period {m(per):7.0f}"
           f"  (slab0 wait {rows[0][1] - rows[0][0]})")
+ph = [[buf[8 * 40 * 4 + w * 6 + j] for j in range(6)] for w in range(8)]
+for w in range(8):
+    p = ph[w]
+    clk = (p[3] - p[0]) / max(1, p[5] - p[4]) * 100.0  # MHz: memtime ticks per 10 ns
+    print(f"wave {w}: bias table {p[1] - p[0]:7d}  to loop end {p[2] - p[1]:8d}  epilogue {p[3] - p[2]:7d}"
+          f"  total {p[3] - p[0]:8d} ticks  clock {clk:6.0f} MHz")
