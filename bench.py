@@ -216,10 +216,12 @@ def wino_exec_ratio(eng):
     direct = 3.0 * 14.0 / 13.5 * pad
     num = den = 0.0
     for l, L in enumerate(eng.levels):
-        f = L.h * L.w * sum(b.geom.flops_per_pixel(True) for b in eng.couple[l] + [eng.prior[l]])
-        dx = eng.conv_mode == "dx3" and eng._dx3_level(l)
-        num += f * (direct if dx else 3.0 * wino)
-        den += f
+        for b in eng.couple[l] + [eng.prior[l]]:
+            g, nd = b.geom, eng.dx3_layers(l, b.geom)
+            for i, gr in enumerate(g.growth):  # the layer's 3x3 FLOPs per pixel ~ c_in x g
+                f = L.h * L.w * (g.a + sum(g.growth[:i])) * gr
+                num += f * (direct if i < nd else 3.0 * wino)
+                den += f
     return num / den
 
 
@@ -450,9 +452,10 @@ def conv_algorithmic_bytes(eng, B):
         cached = L.prior_x_zero and not eng.conditional
         for geom in [b.geom for b in eng.couple[l]] + ([] if cached else [eng.prior[l].geom]):
             c = geom.a
-            # weights per (c, g): 16 Winograd positions or 9 direct taps, as f16 (hi, lo) pairs
-            npos = 9 if (eng.conv_mode == "dx3" and eng._dx3_level(l)) else 16
-            for g in geom.growth:
+            nd = eng.dx3_layers(l, geom)
+            for i, g in enumerate(geom.growth):
+                # weights per (c, g): 16 Winograd positions or 9 direct taps, f16 (hi, lo) pairs
+                npos = 9 if i < nd else 16
                 n += 1
                 byt += 4 * P * (c + g) + npos * c * g * 4
                 c += g

@@ -625,15 +625,21 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
     if (rc) return rc;
   }
   // dx3 blocks keep the split copy of their feature columns (conv3_dx3.hip) at the front of
-  // tmp: the block input is split once here, every layer writes its outputs in both forms
+  // tmp: the block input is split once here, every dx3 layer writes its outputs in both
+  // forms.  The layers with dx3 weights are a prefix (the narrow ones, packing.py
+  // pack_dense_block dx3_cmax); the rest run on wx3, whose workspace then reuses the copy.
   bool dx3 = blk->fold && blk->wx3 && blk->dx3 && !blk->bf16 &&
              idf_conv3x3_dx3_supported(H, W, blk->g_pad);
-  for (int i = 0; dx3 && i < blk->depth; ++i) dx3 = blk->dx3_w[i] != nullptr;
+  int n_dx3 = 0;
+  while (dx3 && n_dx3 < blk->depth && blk->dx3_w[n_dx3]) ++n_dx3;
+  for (int i = n_dx3; dx3 && i < blk->depth; ++i)
+    if (blk->dx3_w[i]) return IDF_ERR_ARG;  // not a prefix
+  dx3 = dx3 && n_dx3 > 0;
   uint16_t* xs = nullptr;
   int32_t nslab_xs = 0;
   if (dx3) {
     nslab_xs = (int32_t)std::min<int64_t>(ld_tmp / 16, ((int64_t)blk->k_in[blk->depth] + 15) / 16);
-    if (blk->depth < 1 || nslab_xs < (blk->k_in[blk->depth - 1] + 15) / 16) return IDF_ERR_WORKSPACE;
+    if (nslab_xs < (blk->k_in[n_dx3 - 1] + 15) / 16) return IDF_ERR_WORKSPACE;
     xs = (uint16_t*)tmp;
     int rc = idf_dx3_split_cols(stream, P, 0, blk->k_in[0], feat, ld_feat, xs, nslab_xs,
                                 blk->range_flag);
@@ -652,7 +658,7 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
                                       blk->b3[i], blk->vtap[i], blk->ldv, blk->bfull[i],
                                       blk->g_pad, feat + c, ld_feat, f16 + c, ld16, n16,
                                       blk->act, blk->slope, ws, ws_floats)
-               : dx3
+               : (dx3 && i < n_dx3)
                    ? idf_conv3x3_dx3(stream, B, H, W, c, xs, nslab_xs, blk->dx3_w[i],
                                      (blk->g_pad + 15) / 16, blk->dx3_yscale[i], blk->b3[i],
                                      blk->vtap[i], blk->ldv, blk->bfull[i], blk->g_pad, feat + c,
@@ -661,7 +667,8 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
                    ? idf_conv3x3_wx3(stream, B, H, W, c, feat, ld_feat, blk->wx3_u[i],
                                      blk->wino_nft, blk->wx3_yscale[i], blk->b3[i], blk->vtap[i],
                                      blk->ldv, blk->bfull[i], blk->g_pad, feat + c, ld_feat,
-                                     blk->act, blk->slope, blk->range_flag, i == 0 ? 1 : 0, tmp,
+                                     blk->act, blk->slope, blk->range_flag,
+                                     (i == 0 || (dx3 && i == n_dx3)) ? 1 : 0, tmp,
                                      P * ld_tmp)
                : wino
                    ? idf_conv3x3_wino(stream, B, H, W, c, feat, ld_feat, blk->wino_u[i],

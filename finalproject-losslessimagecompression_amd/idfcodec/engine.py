@@ -229,13 +229,14 @@ class FlowEngine:
             self.couple.append([DeviceBlock(pack_dense_block(
                 sd, f"blocks.{l}.flows.{2 * k + 1}.dense.", c_depth, c_act, fold=self.fold,
                 wino=self.wino, bf16=self.precision == "bf16", wx3=self.wx3,
-                dx3=self.dx3 and self._dx3_level(l)),
+                dx3=self.dx3 and self._dx3_level(l), dx3_cmax=self._dx3_cmax(l)),
                 self.device) for k in range(self.nflows)])
             self.prior.append(DeviceBlock(pack_dense_block(sd, f"blocks.{l}.prior.NN.", p_depth,
                                                            p_act, fold=self.fold, wino=self.wino,
                                                            bf16=self.precision == "bf16",
                                                            wx3=self.wx3,
-                                                           dx3=self.dx3 and self._dx3_level(l)),
+                                                           dx3=self.dx3 and self._dx3_level(l),
+                                                           dx3_cmax=self._dx3_cmax(l)),
                                           self.device))
             ids_l, inv_l = [], []
             for k in range(self.nflows + 1):
@@ -273,6 +274,23 @@ class FlowEngine:
     def _dx3_level(self, l: int) -> bool:
         Lv = self.levels[l]
         return bool(lib().idf_conv3x3_dx3_supported(Lv.h, Lv.w, 48))
+
+    def _dx3_cmax(self, l: int):
+        """Widest (16-padded) layer input level l runs on dx3 (None: every layer); wider layers
+        of a block run on wx3.  A function of the level geometry only, never of the batch, so
+        an encoder and a decoder of the same model pick the same arithmetic for every layer.
+        Every layer: the same-box bench A/B (profiles/r04/dx3_prefix/bench_ab.txt) measured
+        all-dx3 19.18/19.08 Mpx/s against 18.59/18.76 for dx3 up to 232/152 input channels at
+        32x32/16x16 and 18.41/18.50 for none, although the isolated-launch sweep there has wx3
+        ahead from ~188 channels."""
+        return None
+
+    def dx3_layers(self, l: int, geom) -> int:
+        """Leading layers of a level-l block with geometry `geom` that run on dx3."""
+        if not (self.conv_mode == "dx3" and self._dx3_level(l)):
+            return 0
+        cm = self._dx3_cmax(l)
+        return sum(1 for i in range(geom.depth) if cm is None or geom.k_in[i] <= cm)
 
     def set_conv_mode(self, mode: str):
         """'dx3' (split-f16 direct conv where the geometry allows, split-f16 Winograd

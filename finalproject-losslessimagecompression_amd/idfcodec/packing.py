@@ -251,11 +251,14 @@ def interior_bias(b3: np.ndarray, v: np.ndarray) -> np.ndarray:
 
 def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
                      slope: float = 0.01, fold: bool = False, wino: bool = False,
-                     bf16: bool = False, wx3: bool = False, dx3: bool = False) -> PackedBlock:
+                     bf16: bool = False, wx3: bool = False, dx3: bool = False,
+                     dx3_cmax: int | None = None) -> PackedBlock:
     """Pack the reference DenseBlock parameters found under `prefix` in `sd`
     (keys `{prefix}layers.{i}.layers.{0,1}.{weight,bias}`, head `{prefix}layers.{depth}.*`).
     fold=True folds each layer's 1x1 conv into its 3x3 conv (fold_layer); dx3=True also packs
-    the split-f16 direct-conv weights (dx3_weights) of every folded layer."""
+    the split-f16 direct-conv weights (dx3_weights) of the folded layers whose 16-padded input
+    width is at most dx3_cmax (None: every layer) -- a prefix of the block, since the input
+    widens layer by layer; the remaining layers run on wx3 (flow_kernels.hip dense_block_run)."""
     def arr(k):
         v = sd[prefix + k]
         if hasattr(v, "detach"):
@@ -298,7 +301,7 @@ def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
             if wino or dx3:
                 w64 = np.zeros((g_alloc, 9, ldw3), np.float64)
                 w64[:g][:, :, pos] = wf64
-            if dx3:
+            if dx3 and (dx3_cmax is None or k <= dx3_cmax):
                 wd, yd = dx3_weights(w64, k)
                 wds.append(wd)
                 wdy.append(yd)

@@ -196,10 +196,11 @@ typedef struct IdfDenseBlock {
   const uint16_t *wx3_u[IDF_MAX_DEPTH];
   uint32_t *range_flag;
   /* dx3 = 1 (with wx3 = 1): a block whose geometry idf_conv3x3_dx3_supported takes runs
-   * every layer on the split-f16 direct conv (idf_conv3x3_dx3, weights dx3_w[i], yscale
-   * dx3_yscale[i], the same range guard), its split feature copy in the front of tmp; other
-   * geometries keep wx3.  The choice depends on
-   * (H, W, g_pad) only, so an encoder and its decoder make it alike. */
+   * the layers whose dx3_w[i] is set -- a prefix of the block; NULL from some layer on
+   * leaves that layer and the rest on wx3 -- as the split-f16 direct conv (idf_conv3x3_dx3,
+   * yscale dx3_yscale[i], the same range guard), its split feature copy in the front of tmp;
+   * other geometries keep wx3.  The choice depends on (H, W, g_pad) and the packed prefix
+   * only, never on the batch, so an encoder and its decoder make it alike. */
   int32_t dx3;
   float dx3_yscale[IDF_MAX_DEPTH];
   const uint16_t *dx3_w[IDF_MAX_DEPTH];

@@ -132,6 +132,49 @@ def _x3_blocks_teacher_forced(model, eng, lvl, mode, FO, run_device_block):
     print(f"{mode} level {lvl}: worst whole-block {worst_block:.2e}, worst layer {worst_layer:.2e}")
 
 
+@pytest.mark.parametrize("lvl,n_dx3", [(0, 5), (1, 1)])
+def test_imagenet64_dx3_prefix_block(in64, lvl, n_dx3):
+    """A block packed with dx3 weights for its first n_dx3 layers only (pack_dense_block
+    dx3_cmax): dense_block_run runs those on the direct conv over the split copy and the rest
+    on wx3 (which reuses the copy's workspace and range-checks its first input) -- teacher-forced
+    against flow_oracle and fp64 per layer at 1e-5, re-runs and batch slices bit-exact."""
+    import flow_oracle as FO
+    from idfcodec.engine import DeviceBlock
+    from idfcodec.modules import run_device_block
+    from idfcodec.packing import pack_dense_block
+    model, eng = in64
+    mod = model.blocks[lvl]["flows"][1].dense
+    geom0 = eng.couple[lvl][0].geom
+    sd_full = model.state_dict()
+    pk = pack_dense_block(sd_full, f"blocks.{lvl}.flows.1.dense.", mod.depth, mod.act_name,
+                          fold=True, wino=True, wx3=True, dx3=True,
+                          dx3_cmax=geom0.k_in[n_dx3 - 1])
+    assert len(pk.dx3_w) == n_dx3
+    db = DeviceBlock(pk, torch.device("cuda"))
+    db.desc.range_flag = eng.range_flag.data_ptr()
+    assert db.desc.dx3 == 1
+    hw = eng.levels[lvl].h
+    g = torch.Generator().manual_seed(400 + lvl)
+    x = _grid((3, mod.i_channel, hw, hw), g)
+    sd = {k: v.detach().cpu() for k, v in mod.state_dict().items()}
+    eng.clear_range_flag()
+    out, feat = run_device_block(db, x.cuda(), return_feat=True)
+    torch.cuda.synchronize()
+    assert not eng.range_flag_tripped()
+    assert scaled_err(out, FO.dense_block(x, sd, "", mod.depth, mod.act_name)) <= TOL
+    featc = feat.cpu()
+    for i in range(mod.depth):
+        el = scaled_err(_layer_out(featc, db.geom, i),
+                        _layer_ref_fp64(featc, db.geom, sd, i, hw, hw, mod.act_name))
+        assert el <= TOL, ("layer", i, el)
+    # the all-dx3 and the all-wx3 packings of the same block give other roundings: the
+    # prefix block is its own arithmetic, and deterministic
+    again, _ = run_device_block(db, x.cuda())
+    assert torch.equal(again, out)
+    part, _ = run_device_block(db, x[1:3].contiguous().cuda())
+    assert torch.equal(part, out[1:3])
+
+
 def test_imagenet64_x3_blocks_realistic_inputs(in64):
     """The level-0 couplings on the activations the codec actually feeds them (a forward of
     real synthetic images, captured from the engine's coupling inputs) -- the grid inputs

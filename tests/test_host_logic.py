@@ -315,6 +315,39 @@ def test_bf16_weight_packing_layout():
                 assert np.array_equal(back[s, :, kb, :, e].T, want)
 
 
+def test_dx3_weight_packing_layout_and_prefix(golden):
+    """dx3_weights: [slab][hi, lo][tap][nft][out][ch] f16 pairs with (hi + lo) 2^-k equal to
+    the float64 weight within f16-pair precision, zeros past C; pack_dense_block(dx3_cmax)
+    packs them for the leading layers whose input is at most dx3_cmax wide, nothing after."""
+    import numpy as np
+    from idfcodec.packing import dx3_weights, pack_dense_block
+    rng = np.random.default_rng(6)
+    n_alloc, C, ldw = 48, 40, 48
+    w = rng.normal(0, 0.05, (n_alloc, 9, ldw))
+    w[:, :, C:] = 0
+    d, ysc = dx3_weights(w, C)
+    assert d.shape == (3, 2, 9, 3, 16, 16) and d.dtype == np.uint16
+    f = d.view(np.float16).astype(np.float64)
+    back = (f[:, 0] + f[:, 1]) * ysc                       # slab, tap, nft, out, ch
+    back = back.transpose(2, 3, 1, 0, 4).reshape(n_alloc, 9, 48)
+    assert np.abs(back[:, :, :C] - w[:, :, :C]).max() <= 2.0 ** -20 * np.abs(w).max()
+    assert not back[:, :, C:].any()
+    g = golden("flow_t1_idflows_2lvl.npz")
+    cfg = yaml.safe_load(bytes(g["cfg_yaml"]).decode())
+    sd = {k[3:]: torch.from_numpy(g[k]) for k in g.files if k.startswith("sd/")}
+    depth = cfg["couple"]["nn"]["depth"]
+    assert depth >= 3
+    pre = "blocks.0.flows.1.dense."
+    full = pack_dense_block(sd, pre, depth, fold=True, wino=True, wx3=True, dx3=True)
+    assert len(full.dx3_w) == depth
+    k_in = full.geom.k_in
+    part = pack_dense_block(sd, pre, depth, fold=True, wino=True, wx3=True, dx3=True,
+                            dx3_cmax=k_in[1])
+    assert len(part.dx3_w) == 2
+    for a, b in zip(part.dx3_w, full.dx3_w):
+        assert np.array_equal(a, b)
+
+
 def test_bitstream_conv_flag_round_trips():
     import torch
     from idfcodec.codec import Bitstream
