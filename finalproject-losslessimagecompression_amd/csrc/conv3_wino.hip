@@ -1134,14 +1134,18 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
 #pragma unroll
   for (int j = 0; j < NF; ++j) {
     if constexpr (REGS) {
-      // a wave's two positions are adjacent: one 8-B write per (tile fragment, row)
+      // a wave's two positions are adjacent: one 8-B write per (tile fragment, row).  Tiles
+      // with bit 2 set keep position p in slot p ^ 2, so the two 16-lane halves of each
+      // 32-lane write phase (tiles 4 apart: 80 floats, 16 banks) land on disjoint bank pairs
+      // ({4k, 4k+1} and {4k+2, 4k+3}) -- without the swap they shared them, 2-way conflicts.
+      const int slot = (2 * wave) ^ (2 * ((lane >> 4) & 1));
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int t = 16 * i + (lane >> 4) * 4 + r;
           typedef float f2s __attribute__((ext_vector_type(2)));
-          *(f2s*)(Ms + lr * ERW + t * TPI_ + 2 * wave) = f2s{acc[i][j][r], acc[i][NF + j][r]};
+          *(f2s*)(Ms + lr * ERW + t * TPI_ + slot) = f2s{acc[i][j][r], acc[i][NF + j][r]};
         }
     } else {
 #pragma unroll
@@ -1165,11 +1169,13 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
       if (e_img[it] < g.IMGS && n < g.N) {
         float m[4][4];
         if constexpr (REGS) {
+          // tile bit 2 = wave bit 0 here: the slot swap above undone wave-uniformly
+          const bool swp = (wave & 1) != 0;
 #pragma unroll
           for (int a = 0; a < 4; ++a) {
             const w4 row = *(const w4*)(Ms + nn * ERW + t * TPI_ + 4 * a);
 #pragma unroll
-            for (int b = 0; b < 4; ++b) m[a][b] = row[b];
+            for (int b = 0; b < 4; ++b) m[a][b] = swp ? row[b ^ 2] : row[b];
           }
         } else {
 #pragma unroll

@@ -12,9 +12,9 @@
 // L1/L2), the reduction order depends only on the weights' shape, and the epilogue fuses
 // bias, an optional residual add (ResBlock: act(x + conv)) and the activation.
 //
-// The vector quantiser (roundlib.py:56-62) is one fused kernel: a block keeps 64 latent
-// rows resident in LDS, streams the codebook through MFMA tiles and keeps a running
-// (distance, index) minimum per row -- the [rows x 16384] distance matrix never exists.
+// The vector quantiser (roundlib.py:56-62) is one fused kernel: a block streams 64 latent
+// rows and a slice of the codebook through MFMA tiles and keeps a running (distance, index)
+// minimum per row -- the [rows x 16384] distance matrix never exists.
 // Distances are formed as the reference does, d = (|x|^2 + |e|^2) - 2 x.e in fp32, and
 // ties go to the lowest index (torch.argmin).
 #include <hip/hip_runtime.h>
@@ -206,115 +206,193 @@ static int launch_taps(ConvTapsArgs a, hipStream_t s) {
 // ---------------------------------------------------------------- vector quantiser
 // rows [P][ldx] (D columns), codebook E [K][lde], enorm[k] = |e_k|^2 (fp32, sum in index
 // order).  idx[p] = argmin_k ((|x|^2 + enorm[k]) - 2 x.e_k), lowest k on ties.
-constexpr int kVqBM = 64, kVqBN = 64, kVqMaxD = 512;
+//
+// Block = 4 waves over 64 rows x 128 codes per code tile (wave: 32 rows x 64 codes, 2 x 4
+// accumulator fragments of v_mfma_f32_16x16x4_f32); rows and codes stream through LDS in
+// 16-deep k-chunks (two stages, the next chunk's global loads in flight during the current
+// chunk's 32 MFMAs), so three blocks share a CU.  Blocks split the codebook into S slices:
+// block b takes slice b % S (consecutive blocks land on different XCDs, so an XCD keeps its
+// slice of E in its own L2) and row tile b / S; slices' (distance, index) minima are merged
+// in slice order by vq_argmin_merge_kernel.  Per (row, code) the MFMA chain is the same for
+// every S: k-chunk c, step t, lane group g multiplying k = 16c + 4g + t -- the index is
+// independent of the launch shape.
+constexpr int kVqBM = 64, kVqBN = 128, kVqBK = 16, kVqPitch = kVqBK + 8;
+constexpr int kVqMaxSlices = 8;
+
+__device__ __forceinline__ bool vq_better(float d, int k, float bd, int bk) {
+  return d < bd || (d == bd && k < bk);  // NaN never wins
+}
 
 __global__ void __launch_bounds__(256) vq_argmin_kernel(int64_t P, int32_t D, const float* __restrict__ X,
                                                         int64_t ldx, const float* __restrict__ E,
                                                         int32_t lde, int32_t K,
-                                                        const float* __restrict__ enorm,
+                                                        const float* __restrict__ enorm, int32_t S,
+                                                        int32_t slice_codes,
+                                                        float* __restrict__ part_d,
+                                                        int32_t* __restrict__ part_i,
                                                         int32_t* __restrict__ idx) {
-  constexpr int APITCH = kVqMaxD + 4;  // rows 4 dwords apart: conflict-free fragment reads
-  constexpr int BK = 16, BLD = BK + 8;
-  __shared__ __attribute__((aligned(16))) float As[kVqBM * APITCH];
-  __shared__ __attribute__((aligned(16))) float Bs[2][kVqBN][BLD];
+  __shared__ __attribute__((aligned(16))) float As[2][kVqBM][kVqPitch];
+  __shared__ __attribute__((aligned(16))) float Bs[2][kVqBN][kVqPitch];
   __shared__ float x2s[kVqBM];
-  __shared__ float bestv[4][kVqBM];
-  __shared__ int besti[4][kVqBM];
+  __shared__ float red_d[kVqBM];
+  __shared__ int red_i[kVqBM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t m0 = (int64_t)blockIdx.x * kVqBM;
-  // stage the block's rows (zero beyond P / D)
-  const int dq = (D + 3) / 4;
-  for (int f = tid; f < kVqBM * (kVqMaxD / 4); f += 256) {
-    const int r = f / (kVqMaxD / 4), q = f - r * (kVqMaxD / 4);
-    const int64_t p = m0 + r;
-    f4 v = f4{0.f, 0.f, 0.f, 0.f};
-    if (p < P && q < dq) v = *(const f4*)(X + p * ldx + 4 * q);
-    *(f4*)&As[r * APITCH + 4 * q] = v;
-  }
-  __syncthreads();
-  if (tid < kVqBM) {  // |x|^2 in index order
-    float s = 0.0f;
-    for (int c = 0; c < D; ++c) s = __builtin_fmaf(As[tid * APITCH + c], As[tid * APITCH + c], s);
-    x2s[tid] = s;
-  }
-  // each wave: 16 rows (wave) x 64 codes per tile (4 n-fragments)
+  const int wr = wave & 1, wc = wave >> 1;
+  const int slice = (int)(blockIdx.x % (unsigned)S);
+  const int64_t m0 = (int64_t)(blockIdx.x / (unsigned)S) * kVqBM;
+  const int kb = slice * slice_codes;
+  const int ke = kb + slice_codes < K ? kb + slice_codes : K;
   const int lr = lane & 15, lk = 4 * (lane >> 4);
-  const int nkc = (D + BK - 1) / BK;
-  float best[4];
-  int bidx[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    best[r] = __builtin_inff();
-    bidx[r] = 0x7fffffff;
-  }
-  f4 rb;
-  auto load_b = [&](int k0, int kc) {
-    const int n = tid >> 2, q = tid & 3;
-    const int c = kc * BK + 4 * q;
-    rb = (k0 + n < K && c < D) ? *(const f4*)(E + (int64_t)(k0 + n) * lde + c) : f4{0.f, 0.f, 0.f, 0.f};
+  const int nkc = (D + kVqBK - 1) / kVqBK;
+  // staging: A chunk 64 x 16 = one f4 per thread, B chunk 128 x 16 = two
+  const int ar = tid >> 2, aq = 4 * (tid & 3);
+  f4 ra, rb0, rb1;
+  auto load = [&](int k0, int kc) {
+    const int c = kc * kVqBK + aq;
+    const int64_t p = m0 + ar;
+    ra = (p < P && c < D) ? *(const f4*)(X + p * ldx + c) : f4{0.f, 0.f, 0.f, 0.f};
+    const int n0 = k0 + ar, n1 = k0 + 64 + ar;
+    rb0 = (n0 < ke && c < D) ? *(const f4*)(E + (int64_t)n0 * lde + c) : f4{0.f, 0.f, 0.f, 0.f};
+    rb1 = (n1 < ke && c < D) ? *(const f4*)(E + (int64_t)n1 * lde + c) : f4{0.f, 0.f, 0.f, 0.f};
   };
-  __syncthreads();
-  for (int k0 = 0; k0 < K; k0 += kVqBN) {
-    f4 acc[4];
+  auto store = [&](int buf) {
+    *(f4*)&As[buf][ar][aq] = ra;
+    *(f4*)&Bs[buf][ar][aq] = rb0;
+    *(f4*)&Bs[buf][64 + ar][aq] = rb1;
+  };
+  float best[2][4];
+  int bidx[2][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = f4{0.f, 0.f, 0.f, 0.f};
-    load_b(k0, 0);
-    *(f4*)&Bs[0][tid >> 2][4 * (tid & 3)] = rb;
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      best[i][r] = __builtin_inff();
+      bidx[i][r] = 0x7fffffff;
+    }
+  float x2acc = 0.0f;  // thread tid < 64: |x_row|^2 in index order, formed on the first tile
+  bool first = true;
+  for (int k0 = kb; k0 < ke; k0 += kVqBN) {
+    f4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    load(k0, 0);
+    store(0);
     __syncthreads();
     for (int kc = 0; kc < nkc; ++kc) {
       const int buf = kc & 1;
-      if (kc + 1 < nkc) load_b(k0, kc + 1);
-      const f4 fa = *(const f4*)&As[(wave * 16 + lr) * APITCH + kc * BK + lk];
-      f4 fb[4];
+      if (kc + 1 < nkc) load(k0, kc + 1);
+      f4 fa[2], fb[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = *(const f4*)&Bs[buf][j * 16 + lr][lk];
+      for (int i = 0; i < 2; ++i) fa[i] = *(const f4*)&As[buf][wr * 32 + i * 16 + lr][lk];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = *(const f4*)&Bs[buf][wc * 64 + j * 16 + lr][lk];
+      if (first && tid < kVqBM) {
+        const int cn = D - kc * kVqBK < kVqBK ? D - kc * kVqBK : kVqBK;
+        for (int c = 0; c < cn; ++c) x2acc = __builtin_fmaf(As[buf][tid][c], As[buf][tid][c], x2acc);
+      }
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[t], fb[j][t], acc[j], 0, 0, 0);
-      if (kc + 1 < nkc) *(f4*)&Bs[buf ^ 1][tid >> 2][4 * (tid & 3)] = rb;
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][t], fb[j][t], acc[i][j], 0, 0, 0);
+      if (kc + 1 < nkc) store(buf ^ 1);
       __syncthreads();
     }
-    // lane holds rows wave*16 + (lane>>4)*4 + r, code k0 + j*16 + (lane&15)
+    if (first) {
+      if (tid < kVqBM) x2s[tid] = x2acc;
+      __syncthreads();
+      first = false;
+    }
+    // lane holds rows wr*32 + i*16 + (lane>>4)*4 + r, code k0 + wc*64 + j*16 + (lane&15)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int k = k0 + j * 16 + lr;
-      if (k >= K) continue;
+      const int k = k0 + wc * 64 + j * 16 + lr;
+      if (k >= ke) continue;
       const float en = enorm[k];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float x2 = x2s[wave * 16 + (lane >> 4) * 4 + r];
-        const float d = (x2 + en) - 2.0f * acc[j][r];
-        if (d < best[r] || (d == best[r] && k < bidx[r])) {
-          best[r] = d;
-          bidx[r] = k;
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x2 = x2s[wr * 32 + i * 16 + (lane >> 4) * 4 + r];
+          const float d = (x2 + en) - 2.0f * acc[i][j][r];
+          if (vq_better(d, k, best[i][r], bidx[i][r])) {
+            best[i][r] = d;
+            bidx[i][r] = k;
+          }
+        }
+    }
+  }
+  // reduce over the 16 lanes sharing each row (lanes differ in code column), then the two
+  // waves sharing each row (code halves)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const float ov = __shfl_xor(best[i][r], o);
+        const int oi = __shfl_xor(bidx[i][r], o);
+        if (vq_better(ov, oi, best[i][r], bidx[i][r])) {
+          best[i][r] = ov;
+          bidx[i][r] = oi;
         }
       }
-    }
-  }
-  // reduce over the 16 lanes sharing each row (lanes differ in code column)
+  if (wc == 1 && lr == 0) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      const float ov = __shfl_xor(best[r], o);
-      const int oi = __shfl_xor(bidx[r], o);
-      if (ov < best[r] || (ov == best[r] && oi < bidx[r])) {
-        best[r] = ov;
-        bidx[r] = oi;
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr * 32 + i * 16 + (lane >> 4) * 4 + r;
+        red_d[row] = best[i][r];
+        red_i[row] = bidx[i][r];
       }
-    }
   }
-  if (lr == 0) {
+  __syncthreads();
+  if (wc == 0 && lr == 0) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = wave * 16 + (lane >> 4) * 4 + r;
-      const int64_t p = m0 + row;
-      if (p < P) idx[p] = bidx[r];
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr * 32 + i * 16 + (lane >> 4) * 4 + r;
+        float bd = best[i][r];
+        int bk = bidx[i][r];
+        if (vq_better(red_d[row], red_i[row], bd, bk)) {
+          bd = red_d[row];
+          bk = red_i[row];
+        }
+        const int64_t p = m0 + row;
+        if (p >= P) continue;
+        if (S == 1) {
+          idx[p] = bk;
+        } else {
+          part_d[(int64_t)slice * P + p] = bd;
+          part_i[(int64_t)slice * P + p] = bk;
+        }
+      }
+  }
+}
+
+// the slices' minima in slice order (lowest index on equal distances)
+__global__ void vq_argmin_merge_kernel(int64_t P, int32_t S, const float* __restrict__ part_d,
+                                       const int32_t* __restrict__ part_i, int32_t* __restrict__ idx) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  float bd = part_d[p];
+  int bk = part_i[p];
+  for (int s = 1; s < S; ++s) {
+    const float d = part_d[(int64_t)s * P + p];
+    const int k = part_i[(int64_t)s * P + p];
+    if (vq_better(d, k, bd, bk)) {
+      bd = d;
+      bk = k;
     }
   }
+  idx[p] = bk;
 }
 
 // |e_k|^2 in index order (the reference's torch.sum(weight**2, dim=1) up to summation order)
@@ -472,13 +550,42 @@ int idf_vq_norms(void* stream, int32_t K, int32_t D, const float* e, int32_t lde
   return idf_last_error();
 }
 
+static int vq_slices(int64_t P, int32_t K) {
+  // enough blocks for ~3 per CU on 256 CUs, each slice at least two code tiles
+  const int64_t tiles = (P + kVqBM - 1) / kVqBM;
+  int S = 1;
+  while (S < kVqMaxSlices && tiles * S < 768 && (int64_t)K >= (int64_t)(2 * S) * 2 * kVqBN) S *= 2;
+  return S;
+}
+
+int64_t idf_vq_argmin_workspace_bytes(int64_t P, int32_t K) {
+  const int S = P > 0 && K > 0 ? vq_slices(P, K) : 1;
+  return S > 1 ? (int64_t)S * P * 8 : 0;
+}
+
+int idf_vq_argmin_ws(void* stream, int64_t P, int32_t D, const float* x, int64_t ld_x, const float* e,
+                     int32_t lde, int32_t K, const float* enorm, int32_t* idx, void* ws,
+                     int64_t ws_bytes) {
+  if (P <= 0) return IDF_OK;
+  if (D <= 0 || (D & 3) || (ld_x & 3) || (lde & 3) || K <= 0) return IDF_ERR_ARG;
+  int S = vq_slices(P, K);
+  if (!ws || ws_bytes < (int64_t)S * P * 8) S = 1;  // no room for the slices' minima
+  // codes per slice, whole code tiles (the last slice may be short or empty)
+  const int sc = S == 1 ? K : ((K + S - 1) / S + kVqBN - 1) / kVqBN * kVqBN;
+  float* pd = (float*)ws;
+  int32_t* pi = (int32_t*)(pd + (S > 1 ? (int64_t)S * P : 0));
+  const int64_t blocks = (P + kVqBM - 1) / kVqBM * S;
+  hipLaunchKernelGGL(vq_argmin_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, P, D,
+                     x, ld_x, e, lde, K, enorm, S, sc, pd, pi, idx);
+  if (S > 1)
+    hipLaunchKernelGGL(vq_argmin_merge_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, P, S, pd, pi, idx);
+  return idf_last_error();
+}
+
 int idf_vq_argmin(void* stream, int64_t P, int32_t D, const float* x, int64_t ld_x, const float* e,
                   int32_t lde, int32_t K, const float* enorm, int32_t* idx) {
-  if (P <= 0) return IDF_OK;
-  if (D <= 0 || D > kVqMaxD || (D & 3) || (ld_x & 3) || (lde & 3) || K <= 0) return IDF_ERR_ARG;
-  hipLaunchKernelGGL(vq_argmin_kernel, dim3((unsigned)((P + kVqBM - 1) / kVqBM)), dim3(256), 0,
-                     (hipStream_t)stream, P, D, x, ld_x, e, lde, K, enorm, idx);
-  return idf_last_error();
+  return idf_vq_argmin_ws(stream, P, D, x, ld_x, e, lde, K, enorm, idx, nullptr, 0);
 }
 
 int idf_vq_gather(void* stream, int64_t P, int32_t D, const int32_t* idx, const float* e,

@@ -331,9 +331,11 @@ class VQEngine:
         z, h, w, C, _ = self._guarded(self.enc, x, B, H, W, self.channel)
         assert C == self.D
         idx = torch.empty(B * h * w, dtype=torch.int32, device=self.device)
-        check(lib().idf_vq_argmin(s, B * h * w, self.D, ptr(z), round_up(self.D, 4),
-                                  ptr(self.embed), self.D, self.K, ptr(self.enorm), ptr(idx)),
-              "vq argmin")
+        nws = int(lib().idf_vq_argmin_workspace_bytes(B * h * w, self.K))
+        ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=self.device)
+        check(lib().idf_vq_argmin_ws(s, B * h * w, self.D, ptr(z), round_up(self.D, 4),
+                                     ptr(self.embed), self.D, self.K, ptr(self.enorm), ptr(idx),
+                                     ptr(ws), nws), "vq argmin")
         return idx, (h, w), z
 
     def decode_pm(self, idx, B, h, w, mode=None):

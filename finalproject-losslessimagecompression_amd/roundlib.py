@@ -70,8 +70,10 @@ class VectorQuantizer(nn.Module):
         en = torch.empty(self.num, dtype=torch.float32, device=x.device)
         check(lib().idf_vq_norms(s, self.num, self.dim, ptr(e), self.dim, ptr(en)), "vq norms")
         idx = torch.empty(x.shape[0], dtype=torch.int32, device=x.device)
-        check(lib().idf_vq_argmin(s, x.shape[0], self.dim, ptr(x), self.dim, ptr(e), self.dim,
-                                  self.num, ptr(en), ptr(idx)), "vq argmin")
+        nws = int(lib().idf_vq_argmin_workspace_bytes(x.shape[0], self.num))
+        ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=x.device)
+        check(lib().idf_vq_argmin_ws(s, x.shape[0], self.dim, ptr(x), self.dim, ptr(e), self.dim,
+                                     self.num, ptr(en), ptr(idx), ptr(ws), nws), "vq argmin")
         return idx
 
     def forward(self, x, beta=0.25, gamma=1.0, require_loss=True):

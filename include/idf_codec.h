@@ -437,8 +437,16 @@ int idf_conv_taps_f32(void *stream, int32_t B, int32_t Hi, int32_t Wi, int32_t C
                       int32_t Ho, int32_t Wo, int32_t osy, int32_t osx, int32_t oy0, int32_t ox0,
                       const float *d_res, int64_t ld_res, int32_t act, float slope);
 /* VectorQuantizer.forward's index (roundlib.py:56-62): enorm[k] = |e_k|^2, then
- * idx[p] = argmin_k ((|x_p|^2 + enorm[k]) - 2 x_p.e_k), lowest k on ties; D <= 512. */
+ * idx[p] = argmin_k ((|x_p|^2 + enorm[k]) - 2 x_p.e_k), lowest k on ties; D, ld_x, lde
+ * multiples of 4.  With a device workspace of idf_vq_argmin_workspace_bytes(P, K) bytes the
+ * codebook is split into slices searched by separate blocks (their minima merged in slice
+ * order); without one (idf_vq_argmin, or ws_bytes too small) one block row-tile searches all
+ * of it.  The index does not depend on the split. */
 int idf_vq_norms(void *stream, int32_t K, int32_t D, const float *d_e, int32_t lde, float *d_enorm);
+int64_t idf_vq_argmin_workspace_bytes(int64_t P, int32_t K);
+int idf_vq_argmin_ws(void *stream, int64_t P, int32_t D, const float *d_x, int64_t ld_x,
+                     const float *d_e, int32_t lde, int32_t K, const float *d_enorm, int32_t *d_idx,
+                     void *d_ws, int64_t ws_bytes);
 int idf_vq_argmin(void *stream, int64_t P, int32_t D, const float *d_x, int64_t ld_x,
                   const float *d_e, int32_t lde, int32_t K, const float *d_enorm, int32_t *d_idx);
 /* nn.Embedding lookup: out[p, c] = e[idx[p], c], c < D. */

@@ -126,3 +126,39 @@ def test_vq_argmin_config3_codebook():
     ok = (srt[:, 1] - srt[:, 0]) > 1e-3
     assert ok.float().mean() > 0.5
     assert torch.equal(idx[ok], order[ok, 0])
+
+
+@pytest.mark.parametrize("P,K,D", [(8192, 8192, 512), (1000, 1100, 64), (77, 300, 20),
+                                   (19872, 8192, 512)])
+def test_vq_argmin_slices_equal_one_pass(P, K, D):
+    """The codebook split into slices (idf_vq_argmin_ws with its workspace: separate blocks per
+    slice, minima merged in slice order) gives the index of the one-pass search
+    (idf_vq_argmin) bit for bit -- ragged row tiles, a K with a short or empty last slice, an
+    odd D -- and both equal a float64 search wherever the best two codes differ by > 1e-3;
+    ties (duplicated codes) go to the lowest index."""
+    from idfcodec import _lib
+    from idfcodec._lib import check, lib, ptr
+    g = torch.Generator().manual_seed(P + K)
+    x = torch.tanh(torch.randn(P, D, generator=g)).cuda()
+    e = (torch.randn(K, D, generator=g) * 0.5)
+    e[K // 2] = e[K // 3]  # an exact tie: the lower index must win
+    e = e.cuda()
+    s = _lib.stream_ptr()
+    en = torch.empty(K, device="cuda")
+    check(lib().idf_vq_norms(s, K, D, ptr(e), D, ptr(en)), "norms")
+    one = torch.empty(P, dtype=torch.int32, device="cuda")
+    check(lib().idf_vq_argmin(s, P, D, ptr(x), D, ptr(e), D, K, ptr(en), ptr(one)), "argmin")
+    nws = int(lib().idf_vq_argmin_workspace_bytes(P, K))
+    ws = torch.empty(max(nws, 1), dtype=torch.uint8, device="cuda")
+    sl = torch.empty(P, dtype=torch.int32, device="cuda")
+    check(lib().idf_vq_argmin_ws(s, P, D, ptr(x), D, ptr(e), D, K, ptr(en), ptr(sl), ptr(ws), nws),
+          "argmin ws")
+    assert torch.equal(one, sl)
+    if P * K <= 2_000_000:
+        xd, ed = x.cpu().double(), e.cpu().double()
+        d = (xd ** 2).sum(1, keepdim=True) + (ed ** 2).sum(1) - 2 * xd @ ed.t()
+        srt, order = torch.sort(d, dim=1, stable=True)
+        ok = (srt[:, 1] - srt[:, 0]) > 1e-3
+        assert ok.float().mean() > 0.3
+        assert torch.equal(one.cpu().long()[ok], order[ok, 0])
+    assert not (one.cpu() == K // 2).any()  # the duplicate of code K // 3 never wins
