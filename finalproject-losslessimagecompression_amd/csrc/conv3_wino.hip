@@ -1022,6 +1022,12 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
   // REGS staging write of n-fragment j: a wave's two positions are adjacent, two dword writes
   // per (tile fragment, row) that merge into one ds_write2_b32 (an 8-B write needs its values
   // in an adjacent register pair: two v_mov per write from the accumulators)
+  // The staging slot of this lane's two positions (2 wave, 2 wave + 1): channels 8-15 (lane
+  // bit 3) keep position p in slot p ^ 2.  A ds_write_b64 is served 16 lanes at a time, and
+  // the 16 channels' rows are ERW = 4 (mod 32) dwords apart, so channels n and n + 8 hit the
+  // same bank pair without the swap (4-way conflicts per write, tools/native/lds_probe);
+  // with it the 16 lanes cover all 32 banks.  Readers undo the swap in registers.
+  const int stage_slot = (2 * wave) ^ (2 * ((lane >> 3) & 1));
   auto write_regs = [&](auto jc) {
     constexpr int j = decltype(jc)::value;
 #pragma unroll
@@ -1031,12 +1037,12 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
         const int t = 16 * i + (lane >> 4) * 4 + r;
         if constexpr (IDF_EPI_W2) {
           // (the epilogue's barriers wait lgkmcnt(0) before any read of the staging)
-          const uint32_t a = (uint32_t)(uintptr_t)(lds_ptr_t)(Ms + lr * ERW + t * TPI_ + 2 * wave);
+          const uint32_t a = (uint32_t)(uintptr_t)(lds_ptr_t)(Ms + lr * ERW + t * TPI_ + stage_slot);
           const float x0 = acc[i][j][r], x1 = acc[i][NF + j][r];
           asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" :: "v"(a), "v"(x0), "v"(x1) : "memory");
         } else {
           typedef float f2s __attribute__((ext_vector_type(2)));
-          *(f2s*)(Ms + lr * ERW + t * TPI_ + 2 * wave) = f2s{acc[i][j][r], acc[i][NF + j][r]};
+          *(f2s*)(Ms + lr * ERW + t * TPI_ + stage_slot) = f2s{acc[i][j][r], acc[i][NF + j][r]};
         }
       }
   };
@@ -1058,6 +1064,10 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
           } else {
             R[k][0] = *(const w4*)(row); R[k][1] = *(const w4*)(row + 4);
             R[k][2] = *(const w4*)(row + 8);
+            if (v_nq & 2) {  // channel nl + k >= 8: stage_slot's swap undone
+#pragma unroll
+              for (int q = 0; q < 3; ++q) R[k][q] = w4{R[k][q][2], R[k][q][3], R[k][q][0], R[k][q][1]};
+            }
           }
         }
       };
@@ -1134,11 +1144,9 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
 #pragma unroll
   for (int j = 0; j < NF; ++j) {
     if constexpr (REGS) {
-      // a wave's two positions are adjacent: one 8-B write per (tile fragment, row).  Tiles
-      // with bit 2 set keep position p in slot p ^ 2, so the two 16-lane halves of each
-      // 32-lane write phase (tiles 4 apart: 80 floats, 16 banks) land on disjoint bank pairs
-      // ({4k, 4k+1} and {4k+2, 4k+3}) -- without the swap they shared them, 2-way conflicts.
-      const int slot = (2 * wave) ^ (2 * ((lane >> 4) & 1));
+      // a wave's two positions are adjacent: one 8-B write per (tile fragment, row), in slot
+      // stage_slot (channels 8-15 swap the position pairs of each 4-slot row)
+      const int slot = stage_slot;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1169,8 +1177,7 @@ __global__ void __launch_bounds__(kWThreads) conv3_wino_kernel(WinoArgs g) {
       if (e_img[it] < g.IMGS && n < g.N) {
         float m[4][4];
         if constexpr (REGS) {
-          // tile bit 2 = wave bit 0 here: the slot swap above undone wave-uniformly
-          const bool swp = (wave & 1) != 0;
+          const bool swp = ((nn >> 3) & 1) != 0;  // stage_slot's swap undone
 #pragma unroll
           for (int a = 0; a < 4; ++a) {
             const w4 row = *(const w4*)(Ms + nn * ERW + t * TPI_ + 4 * a);
