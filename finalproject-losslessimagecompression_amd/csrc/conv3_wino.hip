@@ -1346,14 +1346,21 @@ static int wino_launch(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
   } else if (!x3) {
     IDF_WINO_NF(kWSlots, false, false)
   } else {
-#define IDF_WX3_TW(chk, twc)                                                                   \
-  hipLaunchKernelGGL((conv3_wino_kernel<3, kWSlots, true, chk, twc>), dim3((unsigned)blocks),   \
+#define IDF_WX3_TW(nf, chk, twc)                                                               \
+  hipLaunchKernelGGL((conv3_wino_kernel<nf, kWSlots, true, chk, twc>), dim3((unsigned)blocks),  \
                      dim3(kWThreads), 0, s, g)
-    // the common tile widths (imagenet64: 32, 16, 8) with compile-time halo offsets
-    const int twc = NF == 3 && (pl.TW == 32 || pl.TW == 16 || pl.TW == 8) ? pl.TW : 0;
-    if (twc == 32) { if (check_in) IDF_WX3_TW(true, 32); else IDF_WX3_TW(false, 32); }
-    else if (twc == 16) { if (check_in) IDF_WX3_TW(true, 16); else IDF_WX3_TW(false, 16); }
-    else if (twc == 8) { if (check_in) IDF_WX3_TW(true, 8); else IDF_WX3_TW(false, 8); }
+    // the common tile widths with compile-time halo offsets: imagenet64's 32, 16, 8 (NF = 3:
+    // 44-48 outputs; NF = 2: the VQ-VAE's 128-512-channel ResBlock convs) and config 5's 24
+    // (27x23 patches, 32-channel couplings)
+    const int twc = (NF == 3 || NF == 2) && (pl.TW == 32 || pl.TW == 16 || pl.TW == 8 ||
+                                            (NF == 2 && pl.TW == 24)) ? pl.TW : 0;
+    if (NF == 3 && twc == 32) { if (check_in) IDF_WX3_TW(3, true, 32); else IDF_WX3_TW(3, false, 32); }
+    else if (NF == 3 && twc == 16) { if (check_in) IDF_WX3_TW(3, true, 16); else IDF_WX3_TW(3, false, 16); }
+    else if (NF == 3 && twc == 8) { if (check_in) IDF_WX3_TW(3, true, 8); else IDF_WX3_TW(3, false, 8); }
+    else if (twc == 32) { if (check_in) IDF_WX3_TW(2, true, 32); else IDF_WX3_TW(2, false, 32); }
+    else if (twc == 16) { if (check_in) IDF_WX3_TW(2, true, 16); else IDF_WX3_TW(2, false, 16); }
+    else if (twc == 8) { if (check_in) IDF_WX3_TW(2, true, 8); else IDF_WX3_TW(2, false, 8); }
+    else if (twc == 24) { if (check_in) IDF_WX3_TW(2, true, 24); else IDF_WX3_TW(2, false, 24); }
     else if (check_in) IDF_WINO_NF(kWSlots, true, true)
     else IDF_WINO_NF(kWSlots, true, false)
 #undef IDF_WX3_TW
