@@ -887,9 +887,16 @@ int idf_rans_encode_streams(void* stream, int64_t nstreams, int64_t nsym, const 
 
 // Streams per block: 4 by default (a quarter of the CUs: decode lanes run beside another
 // lane's convs; alone it measures the same as 1), IDF_DECODE_WPB=1 for one per block.
+// Streams per decode block (IDF_DECODE_WPB = 1, 2 or 4; timing only, the bits never change).
+// Two: the block's four waves (two decoding, two producing) take one SIMD each, so no chain
+// shares its SIMD's issue with a producer -- 215 vs 265 ns per symbol for four streams per
+// block -- while a lane's launch still holds half the CUs one stream per block would
+// (profiles/r04/rans_wpb/: pipelined bench neutral to +1.3%, back-to-back decode 28.7 -> 27.9
+// ms same box).
 static int decode_pairs_per_block() {
   const char* e = getenv("IDF_DECODE_WPB");
-  return (e && atoi(e) == 1) ? 1 : 4;
+  const int v = e ? atoi(e) : 2;
+  return (v == 1 || v == 4) ? v : 2;
 }
 
 // The block-boundary tables live in LDS only (rans_decode_kernel's producer waves): the
@@ -910,6 +917,10 @@ int idf_rans_decode_streams(void* stream, int64_t nstreams, int64_t nsym, const 
   if (workspace_bytes < idf_rans_decode_workspace_bytes(nsym)) return IDF_ERR_WORKSPACE;
   if (decode_pairs_per_block() == 4)
     hipLaunchKernelGGL(rans_decode_kernel<4>, dim3((unsigned)((nstreams + 3) / 4)), dim3(512), 0,
+                       (hipStream_t)stream, nstreams, sym_off, word_off, nwords, words, mean,
+                       scale, init_state, final_state, out, status);
+  else if (decode_pairs_per_block() == 2)
+    hipLaunchKernelGGL(rans_decode_kernel<2>, dim3((unsigned)((nstreams + 1) / 2)), dim3(256), 0,
                        (hipStream_t)stream, nstreams, sym_off, word_off, nwords, words, mean,
                        scale, init_state, final_state, out, status);
   else

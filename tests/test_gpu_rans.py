@@ -258,10 +258,13 @@ def test_decoder_part1_short_chain_exhaustive():
     assert int(bad.item()) == 0
 
 
-def test_decode_stream_stopping_early_leaves_neighbours_exact(oracle):
+@pytest.mark.parametrize("wpb", ["2", "4", "1"])
+def test_decode_stream_stopping_early_leaves_neighbours_exact(oracle, monkeypatch, wpb):
     """A stream whose decode stops on a zero scale (rans.pyx:36 raises ZeroDivisionError) ends
-    its table producer early; the other streams of its block (4 per block) decode on, equal to
-    the oracle."""
+    its table producer early; the other streams of its block (IDF_DECODE_WPB streams per block:
+    2 by default, 4, 1) decode on, equal to the oracle -- every block shape gives the same
+    symbols, states and status."""
+    monkeypatch.setenv("IDF_DECODE_WPB", wpb)
     g = np.random.default_rng(12)
     lens = np.array([300, 700, 130, 900, 64, 65, 1000, 5], np.int64)
     off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
