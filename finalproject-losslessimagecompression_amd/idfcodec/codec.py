@@ -644,11 +644,15 @@ class ImageCodec:
                 # together after the top level (the GPU ran only rANS kernels for 3.7 ms of a
                 # 31 ms decode), but neither "levels", a high-priority lane 0 nor unequal lanes
                 # (IDF_LANE_SPLIT) shortened the decode (profiles/r02/lanes/order_ab.txt).
-                # "flows0" (default): as "top", and at the bottom level lane i's couplings start
-                # when lane i-1's are done, so lane i's longest rANS decode runs beside lane
-                # i-1's couplings (+0.5-0.9% bench, decode -0.2..0.3 ms, same-box A/B x5 over
-                # two boxes: profiles/r03/lanes_flows); "flows" orders every level so (-2.7%).
-                stagger = os.environ.get("IDF_LANE_STAGGER", "flows0")
+                # "flows0": as "top", and at the bottom level lane i's couplings start when lane
+                # i-1's are done, so lane i's longest rANS decode runs beside lane i-1's
+                # couplings (round 3's default: +0.5-0.9% bench with four streams per decode
+                # block, profiles/r03/lanes_flows); "flows" orders every level so (-2.7%).
+                # "top" is the default again since the decode runs two streams per block (a
+                # faster chain, profiles/r04/rans_wpb): back-to-back decode 27.6 vs 28.0 ms,
+                # bench +0.7% pipelined / +1.2% back to back, same box
+                # (profiles/r04/lane_stagger/).
+                stagger = os.environ.get("IDF_LANE_STAGGER", "top")
                 # The host enqueues the lanes interleaved -- one step (a level's rANS decode, or
                 # one coupling) of each lane in turn -- so that every lane's launches reach the
                 # GPU early: enqueued lane after lane, the second lane's first kernel waited for
