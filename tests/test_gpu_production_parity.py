@@ -567,3 +567,37 @@ def test_config3_full_batch_1024(oracle):
     _sampled_streams_vs_oracle(oracle, fl, rbs, seed=5)
     out, info = codec.decode(rbs)
     assert info["ok"] and torch.equal(out, x)
+
+
+def test_bench_config_b256_streams_vs_oracle(oracle, in64):
+    """BASELINE configs[1] at its own batch (imagenet64, B = 256, the bench's workload): the
+    codec's encode in its production mode (dx3 + x3 convs, side-stream level encode, lanes)
+    -- a sample of its 768 (level, image) streams equal the C oracle's encode of the device's
+    own latents / means / scales word for word, and the decode restores the images exactly."""
+    from idfcodec import synthetic
+    model, eng = in64
+    codec = model.codec()
+    B = 256
+    img = synthetic.images(B, seed=31).cuda()
+    bs = codec.encode(img)
+    torch.cuda.synchronize()
+    assert bs.meta.get("conv") == "dx3"
+    ws = eng.workspace(B)
+    lat, mean, scale = (ws[k].cpu().numpy() for k in ("lat", "mean", "scale"))
+    off = codec.coder.sym_off(B).cpu().numpy()
+    st = bs.states.cpu().numpy().view(np.uint64)
+    nw = bs.nwords.cpu().numpy()
+    words = bs.words.cpu().numpy().view(np.uint32)
+    woff = np.concatenate([[0], np.cumsum(nw)[:-1]])
+    ns = off.size - 1
+    assert ns == 3 * B
+    rng = np.random.default_rng(256)
+    pick = np.unique(np.concatenate([[0, B - 1, B, 2 * B - 1, 2 * B, ns - 1],
+                                     rng.integers(0, ns, 26)]))
+    for k in pick:
+        a, b = int(off[k]), int(off[k + 1])
+        rs, rw = oracle.encode(1 << 32, lat[a:b], mean[a:b], scale[a:b])
+        assert int(st[k]) == rs, k
+        assert np.array_equal(words[woff[k]:woff[k] + nw[k]], rw), k
+    out, info = codec.decode(bs)
+    assert info["ok"] and torch.equal(out, img)
