@@ -710,8 +710,6 @@ class ImageCodec:
                     # longest rANS chains, the largest couplings) is ordered so; the others
                     # step round-robin as in "top".
                     flows_done = [None] * nl
-                    lvl_done = [None] * nl
-                    hold = int(os.environ.get("IDF_LANE_HOLD", "0"))
                     for lv in range(eng.nsplit):
                         ordered = stagger == "flows" or top - lv == 0
                         if ordered:
@@ -725,26 +723,11 @@ class ImageCodec:
                                         next(gens[i])
                                     flows_done[i] = torch.cuda.Event()
                                     flows_done[i].record(st)
-                        else:
-                            # lane i's last `held` couplings of this level wait until lane i-1
-                            # has finished the level, so they run beside lane i-1's next-level
-                            # prior and rANS decode (serial chains that fill few CUs) instead of
-                            # beside lane i-1's couplings (IDF_LANE_HOLD, 0 = off)
-                            nsteps = eng.nflows + (1 if lv else 0)
-                            held = min(hold, eng.nflows) if nl > 1 else 0
-                            for k in range(nsteps - held):
+                        else:  # round robin, one step of each lane in turn
+                            for k in range(eng.nflows + (1 if lv else 0)):
                                 for i, st in enumerate(streams):
                                     with torch.cuda.stream(st):
                                         next(gens[i])
-                            if held:
-                                for i, st in enumerate(streams):
-                                    with torch.cuda.stream(st):
-                                        if i:
-                                            st.wait_event(lvl_done[i - 1])
-                                        for k in range(held):
-                                            next(gens[i])
-                                        lvl_done[i] = torch.cuda.Event()
-                                        lvl_done[i].record(st)
                     for i, st in enumerate(streams):
                         with torch.cuda.stream(st):
                             try:
