@@ -34,9 +34,11 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(REPO, "finalproject-losslessimagecompression_amd")
 sys.path.insert(0, PKG)
 # hardware queues per process: the pipelined steps use six HIP streams (the encode's and its
-# rANS side stream, the decode's and its two lanes, the default); with HIP's default of 4 two
-# of them would share a queue and run in order.  Set before anything initialises HIP.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# rANS side stream, the decode's and its two lanes, the default), so with 4 queues some share
+# one and run in order -- measured faster than 8 or 16 queues with the round-4 decode (19.17-
+# 19.32 vs 18.32-18.73 Mpx/s, 5 same-box pairs over two boxes: profiles/r04/hwq/).  Set before
+# anything initialises HIP.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "4")
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
