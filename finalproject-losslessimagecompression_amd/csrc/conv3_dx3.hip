@@ -555,7 +555,12 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
 }
 
 // Block-input split: XS channels [c0, c1) of every pixel from the fp32 rows x (ld_x floats),
-// zeros for [c1, round16(c1)) (the first layer's own output slab: read before it is written);
+// zeros for [c1, round16(c1)) (the first layer's own output slab: other blocks of that
+// layer's launch read it -- as halo -- while its own blocks write it, so the value a reader
+// sees depends on timing; it is only ever multiplied by exactly-zero weights (packing
+// dx3_weights asserts the weights of channels >= C are +0) and every value written there is
+// finite (these zeros, and outputs under the |y| < 8192 guard), so the product is +-0 either
+// way and the sum's bits do not depend on which value was read);
 // ORs bit 0 of flag for a value that is NaN or |x| >= 32768 (the f16 pairs' range).  One
 // thread per (pixel, 4 channels).
 __global__ void __launch_bounds__(256) dx3_split_cols_kernel(int64_t P, int32_t c0, int32_t c1,

@@ -381,16 +381,26 @@ class ImageCodec:
         self.overlap_encode = os.environ.get("IDF_ENC_OVERLAP", "1") == "1"
         self._streams = []
         self.lane_marks = None
+        # resident workspace sets: every decode lane's, the pipelined encode's (ENC_SLOT) and
+        # one more, so a pipelined step never evicts and reallocates a full-batch set
+        if engine is not None:
+            engine.ws_keep = max(engine.ws_keep, max(self.lanes, self.enc_lanes) + 2)
 
-    # engine workspace slot of an encode that may run beside a decode (encode_decode_stream):
-    # the decode lanes hold slots 0 .. lanes - 1
-    ENC_SLOT = 8
+    # engine workspace slot of an encode that may run beside a decode on another stream (the
+    # pipelined steps of bench.py run_steps_pipelined): the decode lanes and encode lanes hold
+    # slots 0 .. lanes - 1, so this key is one no lane uses.  Shared between the two streams
+    # (the caller must not switch conv modes while the other stream still enqueues): the
+    # engine's block descriptors and conv mode (set_conv_mode, host state read at enqueue time),
+    # its range_flag word, and the per-mode top-prior cache (engine._top_prior: kept for the
+    # engine's lifetime, its users wait on the event recorded where it was computed).
+    ENC_SLOT = -1
 
     @torch.no_grad()
     def encode(self, img_u8: torch.Tensor, cond=None, compact: bool = True,
                slot: int = 0) -> Bitstream:
-        """slot: the engine workspace set the flow runs in (a different one from the decode
-        lanes' lets an encode overlap a decode on another stream, encode_decode_stream)."""
+        """slot: the engine workspace set the flow runs in (ENC_SLOT, a different one from the
+        decode lanes', lets an encode overlap a decode on another stream: bench.py
+        run_steps_pipelined; ENC_SLOT's comment lists the state the two share)."""
         _lib.require_device(img_u8, "image batch")
         if img_u8.dtype != torch.uint8:
             raise TypeError("ImageCodec.encode expects uint8 images")

@@ -16,6 +16,7 @@ HBM layout (per batch of B images):
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import os
 from dataclasses import dataclass
@@ -267,8 +268,12 @@ class FlowEngine:
         self.ld_tmp = self.ld_feat
         if self.precision == "bf16":
             self.ld_tmp = max(self.ld_feat, round_up(self.ld_feat, 64) // 2 + 2 * 48 + 8)
-        self._ws = {}
-        self._top_prior = None
+        self._ws = collections.OrderedDict()
+        self.ws_keep = 4
+        # IDFlows' data-independent top prior, one entry per conv mode, never dropped: an
+        # encode on one stream may switch the mode (the range guard's f32 recompute) while a
+        # decode on another still has copies from the current mode's entry queued
+        self._top_prior = {}
 
     # ------------------------------------------------------------ conv mode
     def _dx3_level(self, l: int) -> bool:
@@ -307,8 +312,7 @@ class FlowEngine:
         for b in self._blocks:
             b.desc.wx3 = on if b.wx3_u else 0
             b.desc.dx3 = 1 if (mode == "dx3" and b.dx3_w and b.desc.wx3) else 0
-        self.conv_mode = mode
-        self._top_prior = None  # computed under the previous mode
+        self.conv_mode = mode  # each mode's top prior is cached separately (_top_prior)
 
     @property
     def conv_family(self) -> str:
@@ -354,9 +358,11 @@ class FlowEngine:
     # ------------------------------------------------------------ workspace
     def workspace(self, B: int, slot: int = 0):
         """Activation / latent buffers for B images.  Each slot is an independent set (the
-        ImageCodec lanes run one slot per HIP stream); the four most recent sets stay resident."""
+        ImageCodec lanes run one slot per HIP stream); the ws_keep most recently used sets stay
+        resident (ImageCodec raises ws_keep to its lanes + the pipelined encode's slot + 1)."""
         ws = self._ws.get((B, slot))
         if ws is not None:
+            self._ws.move_to_end((B, slot))  # least recently used goes first
             return ws
         dev = self.device
         f = lambda n: torch.empty(int(n), dtype=torch.float32, device=dev)  # noqa: E731
@@ -377,7 +383,7 @@ class FlowEngine:
             # channels C..3 of the 4-wide pixel rows stay zero (they meet zero weights)
             ws["cond_img"] = torch.zeros(B * self.H * self.W * 4, dtype=torch.float32, device=dev)
         # the last few sets stay resident (an encode batch plus the decode lanes' sub-batches)
-        while len(self._ws) >= 4:
+        while len(self._ws) >= max(1, self.ws_keep):
             self._ws.pop(next(iter(self._ws)))
         self._ws[(B, slot)] = ws
         return ws
@@ -439,22 +445,30 @@ class FlowEngine:
         """Computes the cached top prior on stream s if it is needed and missing (the lanes
         call this on their parent stream before forking, so no lane races its creation)."""
         Lv = self.levels[-1]
-        if self._top_prior is None and Lv.prior_x_zero and not self.conditional:
+        if self.conv_mode not in self._top_prior and Lv.prior_x_zero and not self.conditional:
             self._top_prior_cached(ws, 0, s, 0)
 
     def _top_prior_cached(self, ws, B, s, off):
         """IDFlows' top prior sees zeros (priorlib.py:43): its output does not depend on
-        the data, so it is computed once (batch 1) and replicated per image."""
+        the data, so it is computed once per conv mode (batch 1) and replicated per image;
+        the entry lives as long as the engine (see __init__)."""
         Lv = self.levels[-1]
         n = Lv.n_sym
-        if self._top_prior is None:
-            tp = torch.empty(3 * n, dtype=torch.float32, device=self.device)
+        hit = self._top_prior.get(self.conv_mode)
+        if hit is None:
+            t = torch.empty(3 * n, dtype=torch.float32, device=self.device)
             ws1 = {"feat": ws["feat"], "tmp": ws["tmp"]}
-            self._prior(ws1, 1, self.nsplit - 1, s, ptr(tp), ptr(tp) + n * FLOAT,
-                        ptr(tp) + 2 * n * FLOAT)
-            self._top_prior = tp.view(3, n)
+            self._prior(ws1, 1, self.nsplit - 1, s, ptr(t), ptr(t) + n * FLOAT,
+                        ptr(t) + 2 * n * FLOAT)
+            made = torch.cuda.Event()
+            made.record()  # the stream it was computed on (current: s)
+            hit = self._top_prior[self.conv_mode] = (t.view(3, n), made)
+        tp, made = hit
+        # a user on another stream (the other side of a pipelined encode / decode) waits for
+        # the computation, wherever it was enqueued
+        torch.cuda.current_stream(self.device).wait_event(made)
         for i, key in enumerate(("mean", "logscale", "scale")):
-            ws[key][off: off + B * n].view(B, n).copy_(self._top_prior[i].expand(B, n))
+            ws[key][off: off + B * n].view(B, n).copy_(tp[i].expand(B, n))
 
     # ------------------------------------------------------------ forward
     @torch.no_grad()

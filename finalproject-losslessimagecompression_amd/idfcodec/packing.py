@@ -222,6 +222,11 @@ def dx3_weights(w: np.ndarray, C: int):
     for t, part in enumerate((hi, lo)):
         p = part.view(np.uint16).reshape(nft, 16, 9, nslab, 16)  # f, r, tap, slab, c
         out[:, t] = p.transpose(3, 2, 0, 1, 4)
+    # The kernel's invariant (conv3_dx3.hip, "split copy"): a layer reads its input's last slab
+    # up to the next multiple of 16 channels, i.e. also channels [C, 16 nslab) that other
+    # blocks of the same launch are writing (its own outputs).  Those channels must meet
+    # exactly +0 weights (hi and lo), so any finite value there adds exactly +-0.
+    assert C % 16 == 0 or not out[-1, :, :, :, :, C % 16:].any(), "dx3 weights past C not zero"
     return np.ascontiguousarray(out), float(2.0 ** -k)
 
 

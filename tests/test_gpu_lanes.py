@@ -163,3 +163,40 @@ def test_encode_beside_decode_exact():
         assert bool((info_a["final_states"] == 1 << 32).all())
         assert torch.equal(bs_b.states, ref_b.states) and torch.equal(bs_b.nwords, ref_b.nwords)
         assert torch.equal(bs_b.words, ref_b.words) and bs_b.meta["conv"] == ref_b.meta["conv"]
+
+
+def test_encode_fallback_beside_decode_exact(monkeypatch):
+    """The range guard's f32 recompute inside an encode on stream E (forced here) switches the
+    engine's conv mode while batch A's decode on stream D still has queued copies of the dx3
+    top prior: the per-mode top-prior cache keeps that tensor alive, so A decodes exactly and
+    B's bitstream equals B encoded alone in f32."""
+    from idfcodec import _lib, configs, synthetic
+    model = synthetic.build_model(configs.get("imagenet64")).cuda()
+    codec = model.codec()
+    eng = model.engine()
+    a = synthetic.images(32, seed=81).cuda()
+    b = synthetic.images(32, seed=82).cuda()
+    bs_a = codec.encode(a)
+    assert bs_a.meta["conv"] == eng.conv_mode != "f32"
+    mode = eng.conv_mode
+    eng.set_conv_mode("f32")
+    ref_b = codec.encode(b)
+    eng.set_conv_mode(mode)
+    assert ref_b.meta["conv"] == "f32"
+    torch.cuda.synchronize()
+    E, D = _lib.new_stream(), _lib.new_stream()
+    done_a = torch.cuda.Event()
+    done_a.record()
+    monkeypatch.setattr(type(eng), "range_flag_tripped", lambda self: True)
+    for _ in range(2):
+        with torch.cuda.stream(D):
+            D.wait_event(done_a)
+            out_a, info_a = codec.decode(bs_a, verify=False)
+        with torch.cuda.stream(E):
+            bs_b = codec.encode(b, slot=codec.ENC_SLOT)
+        torch.cuda.synchronize()
+        assert eng.conv_mode == mode
+        assert torch.equal(out_a, a)
+        assert bool((info_a["final_states"] == 1 << 32).all())
+        assert bs_b.meta["conv"] == "f32"
+        assert torch.equal(bs_b.states, ref_b.states) and torch.equal(bs_b.words, ref_b.words)
