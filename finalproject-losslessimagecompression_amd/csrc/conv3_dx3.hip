@@ -18,16 +18,30 @@
 // writes its outputs in both forms.  So a slab's halo goes HBM -> LDS by LDS-DMA with no
 // registers, no conversion and no VALU: the k-loop is LDS reads and MFMAs.
 //
-// Block = 8 waves (two per SIMD) = WR/2 16x16 output tiles x NF*16 outputs; a wave owns WR
-// output rows (WR 16-pixel B fragments) of one tile x all outputs.  Per 16-channel slab the
-// block stages into one of two LDS stages, by LDS-DMA issued a slab ahead:
-//   * each tile's 18x18 halo as two planes, xh [324 slots][16] and xl [324 slots][16] (32 B
-//     per slot: every ds_read_b128 lane group of the fragment reads is bank-conflict-free);
+// Output tiles are 16 x 16 "packed" pixels (dx3_plan): images a multiple of 16 wide tile one
+// image; smaller images pack nbx x nby to a tile (imagenet64's 8 x 8 level: 2 x 2 images,
+// config 4's 4 x 4 patches: 4 x 4), and widths that are neither (config 5's 23-wide patches)
+// pack side by side in bands of nbx images, a tile crossing at most one image edge.  The LDS
+// canvas of a tile holds each image's halo in its own SEGMENT with zero gutters, so a lane's
+// 3 x 3 taps never see a neighbouring image: lane j reads canvas slot rowbase * PITCH +
+// colbase(j) + tap, and the segment bases are chosen so colbase(j) = j (mod 8) -- every
+// ds_read_b128 lane group of the fragment reads then still covers 16 distinct bank quads.
+//
+// Block = 8 waves (two per SIMD) = WR/2 tiles x NF*16 outputs (one of ngroup output groups);
+// a wave owns WR output rows (WR 16-pixel B fragments) of one tile x NF fragments.  Per
+// 16-channel slab the block stages into one of two LDS stages, by LDS-DMA issued a slab ahead:
+//   * each tile's canvas as two planes, xh [slots][16] and xl [slots][16] (32 B per slot);
 //   * the slab's weights in A-fragment order, wh [9 taps][NF][16 out][16 ch] then wl.
-// One barrier per slab.  A pixel fragment (16 pixels of one halo row, one tap column) is read
+// One barrier per slab.  A pixel fragment (16 pixels of one canvas row, one tap column) is read
 // once and feeds the 3 output rows x NF fragments that use it.
-// Each output is one fixed-order sum (slabs, then the tap/product order below) whose order
-// depends on C only: batch- and tile-invariant, so encoder and decoder agree bit for bit.
+//
+// Split K (nchunk > 1; dx3_plan: the 8 x 8 level, whose 64 tiles per 256 images cannot fill
+// the chip): the slabs are cut into nchunk fixed chunks, one block each; a block writes its
+// raw accumulators to a partial buffer, and the block that finishes a tile's last chunk (an
+// agent-scope counter per tile, self-resetting) sums the chunks in chunk order and runs the
+// epilogue -- no reduce launch.  Each output is one fixed-order sum (slabs within a chunk, the
+// chunks left to right, the tap/product order below) whose order depends on (H, W, C) only:
+// batch- and tile-invariant, so encoder and decoder agree bit for bit.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -49,11 +63,20 @@ struct Dx3Args {
   int64_t P;           // pixels of the batch (B * H * W)
   int32_t nslab_xs;    // slabs the split buffer holds
   int32_t C;           // input channels (slabs read: ceil(C / 16))
-  const uint16_t* Wt;  // [nslab][2: hi, lo][9 taps][nft][16 out][16 ch] f16 bits of w * 2^k
-  int32_t nslab, nft;
+  const uint16_t* Wt;  // [nslab][ngroup][2: hi, lo][9 taps][NF][16 out][16 ch] f16 of w * 2^k
+  int32_t nslab, ngroup;
   int32_t N;
   int32_t B, H, Wd;
-  int32_t tiles_y, tiles_x, ntiles;
+  // packed tiling (dx3_plan)
+  int32_t nbx, nby;     // images per band across / down
+  int32_t tiles_x, tiles_y, ntiles, nblk_tiles;
+  int32_t ch;           // canvas rows
+  int32_t seg, segw, nseg;  // segment stride and width (slots), segments per canvas
+  int32_t modeb;        // 1: at most two segments side by side in a row (runtime split)
+  // split K
+  int32_t nchunk, chunk_slabs;
+  float* part;          // [nblk_tiles][ngroup][nchunk][waves][WR][NF][64 lanes] d4
+  uint32_t* ctr;        // [nblk_tiles][ngroup], zero at the launch, left zero
   const float* b3;
   const float* vtap;
   const float* bfull;
@@ -125,15 +148,6 @@ __device__ unsigned long long g_dx3_phase[8][6];
 #ifndef IDF_DX3_DMAW0
 #define IDF_DX3_DMAW0 0
 #endif
-// 1: cross-slab prefetch -- two barriers per slab: one at its start (the stage slab s - 1 used
-// may be refilled: slab s + 1's DMA is issued), one at step IDF_DX3_X (slab s + 1's stage is
-// complete: the slab's last steps read slab s + 1's first fragments)
-#ifndef IDF_DX3_XPF
-#define IDF_DX3_XPF 0
-#endif
-#ifndef IDF_DX3_X
-#define IDF_DX3_X 20
-#endif
 // 1: one tile per block at every geometry (timing A/B of the two block shapes)
 #ifndef IDF_DX3_FORCE1
 #define IDF_DX3_FORCE1 0
@@ -145,29 +159,33 @@ __device__ unsigned long long g_dx3_phase[8][6];
 #endif
 constexpr int kDxWaves = IDF_DX3_WAVES;
 constexpr int kDxThreads = 64 * kDxWaves;
-constexpr int kDxCW = 18;                 // halo canvas width (slots) = tile width 16 + 2
-constexpr int kDxSlots = kDxCW * kDxCW;   // 324
-constexpr int kDxPlane = 11 * 1024;       // one plane (xh or xl): 324 x 32 B in whole 1-KiB pieces
-constexpr int kDxPlanePieces = kDxPlane / 1024;
 constexpr uint32_t kDxInvalid = 0xFFFFFFF0u;
 // the split-f16 range guard on stored outputs: |y| < 8192, as wx3 (|x| < 32768 on block inputs
 // is checked where the inputs are split, idf_dx3_split_cols)
 constexpr float kDxInGuard = 32768.0f;
 constexpr float kDxOutGuard = 8192.0f;
 
-template <int NF, int WR>
+// The canvas shapes the library instantiates: (row pitch in slots, plane size in KiB).  18 /
+// 11: one 16-wide tile of one image (18 x 18 halo); 10 / 13: 8-wide images, two segments of
+// 10 x 20 (2 x 2 images of 8 x 8); 6 / 19: 4-wide images, four segments of 6 x 24; 26 / 17:
+// widths with one image edge inside a tile (two segments side by side, the second 8 slots past
+// the first's last lane: colbase = j mod 8).
+template <int NF, int WR, int PITCH, int PLANE_KIB>
 struct Dx3Lds {
-  static constexpr int T = WR * kDxWaves / 16;     // 16x16 tiles per block
-  static constexpr int HR = WR + 2;                // halo rows a wave reads
+  static constexpr int T = WR * kDxWaves / 16;     // tiles per block
+  static constexpr int HR = WR + 2;                // canvas rows a wave reads
   static constexpr int NS = 5 * HR - 1;            // steps per slab (see the schedule)
-  static constexpr int WOFF = T * 2 * kDxPlane;    // weights within a stage
+  static constexpr int PLANE = PLANE_KIB * 1024;   // one plane (xh or xl) of a tile's canvas
+  static constexpr int SLOTS = PLANE / 32;
+  static constexpr int WOFF = T * 2 * PLANE;       // weights within a stage
   static constexpr int WPART = 9 * NF * 512;       // one part (wh or wl) of a slab's weights
   static constexpr int WST = 2 * WPART;            // a multiple of 1 KiB: whole DMA pieces
   static constexpr int STAGE = WOFF + WST;
   static constexpr int ZOFF = 2 * STAGE;           // NF * 512 B of zeros (the odd tap's pair)
   static constexpr int BOFF = ZOFF + NF * 512;     // bias table [16 classes][NF * 16] f32
-  static constexpr int BYTES = BOFF + 16 * NF * 16 * 4;
-  static constexpr int HPIECES = T * 2 * kDxPlanePieces;   // halo DMA pieces per slab
+  static constexpr int FOFF = BOFF + 16 * NF * 16 * 4;  // the split-K "last block" flag
+  static constexpr int BYTES = FOFF + 16;
+  static constexpr int HPIECES = T * 2 * PLANE_KIB;        // halo DMA pieces per slab
   static constexpr int NPIECES = HPIECES + WST / 1024;     // + weight pieces
   static constexpr int PPW = (NPIECES + IDF_DX3_DMAW - 1) / IDF_DX3_DMAW;  // pieces per wave (max)
 };
@@ -180,31 +198,68 @@ __device__ __forceinline__ void dx_unroll(F&& f, std::integer_sequence<int, T...
   (f(std::integral_constant<int, T>{}), ...);
 }
 
-template <int NF, int WR>
+// A tile's place in the packed layout: band (nbx x nby images), first packed column u0 and row
+// u0y, the image column ix0 / row iy0 they fall in, the first column's image x (xf0), the first
+// lane of the next image column (jc; >= 16: none), the canvas row 0's vertical coordinate vy0
+// (canvas row cr holds packed vertical coordinate vy0 + cr, image row vy / (H + 2)).
+struct DxTile {
+  int band, u0, ix0, xf0, jc, u0y, iy0, vy0;
+};
+
+__device__ __forceinline__ DxTile dx_tile(const Dx3Args& g, int tile) {
+  DxTile t;
+  int q = tile;
+  const int tx = q - udiv_s(q, g.tiles_x) * g.tiles_x;
+  q = udiv_s(q, g.tiles_x);
+  const int ty = q - udiv_s(q, g.tiles_y) * g.tiles_y;
+  t.band = udiv_s(q, g.tiles_y);
+  t.u0 = 16 * tx;
+  t.ix0 = udiv_s(t.u0, g.Wd);
+  t.xf0 = t.u0 - t.ix0 * g.Wd;
+  t.jc = (t.ix0 + 1) * g.Wd - t.u0;
+  t.u0y = 16 * ty;
+  t.iy0 = udiv_s(t.u0y, g.H);
+  if (t.iy0 > g.nby - 1) t.iy0 = g.nby - 1;
+  t.vy0 = t.u0y + 2 * t.iy0;
+  return t;
+}
+
+template <int NF, int WR, int PITCH, int PLANE_KIB>
 __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
-  using L = Dx3Lds<NF, WR>;
+  using L = Dx3Lds<NF, WR, PITCH, PLANE_KIB>;
   constexpr int T = L::T, HR = L::HR, NS = L::NS;
   static_assert(L::WST % 1024 == 0, "weight stage must be whole 1-KiB DMA pieces");
   static_assert(L::BYTES <= 160 * 1024, "LDS");
   static_assert(HR >= 3, "the A-fragment reads of a phase take its last three steps");
   __shared__ __attribute__((aligned(16))) char lds[L::BYTES];
+  int* last_flag = (int*)(lds + L::FOFF);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // block -> (chunk, output group, tile block), chunk-major: the blocks of one XCD (a
+  // contiguous range, xcd_contiguous) mostly share a chunk and group, i.e. their weights
   const int bid = xcd_contiguous(blockIdx.x, gridDim.x);
+  const int per_chunk = g.ngroup * g.nblk_tiles;
+  const int chunk = udiv_s(bid, per_chunk);
+  const int rem = bid - chunk * per_chunk;
+  const int grp = udiv_s(rem, g.nblk_tiles);
+  const int tb = rem - grp * g.nblk_tiles;
+  const int s0 = chunk * g.chunk_slabs;
+  const int s1 = min(g.nslab, s0 + g.chunk_slabs);
   // the wave's tile and first output row
   const int tw = wave / (kDxWaves / T);
   const int r0 = WR * (wave % (kDxWaves / T));
-  const int tile = bid * T + tw;
+  const int tile = tb * T + tw;
 
-  // ---- DMA plan: piece k = wave + 8 i of each slab.  Halo pieces k < HPIECES: tile k / 22,
-  // plane (k / 11) % 2, slots 32 (k % 11) .. +31 (lane: slot + lane / 2, 8 channels (lane & 1));
-  // weight pieces: 1 KiB of the slab's weights each.
+  // ---- DMA plan: piece k = wave + 8 i of each slab.  Halo pieces k < HPIECES: tile k /
+  // (2 PLANE_KIB), plane (k / PLANE_KIB) % 2, canvas slots 32 (k % PLANE_KIB) .. +31 (lane:
+  // slot + lane / 2, 8 channels (lane & 1)); weight pieces: 1 KiB of the slab's group weights.
   const int64_t plane_b = g.P * 32;                      // bytes of one plane of one slab
   const uint32_t xs_stride = (uint32_t)(2 * plane_b);    // bytes per slab
   const int64_t xs_bytes = (int64_t)g.nslab_xs * 2 * plane_b;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)g.xs, 0, (int)(xs_bytes < (int64_t)kDxInvalid ? xs_bytes : (int64_t)kDxInvalid), 0x00020000);
-  const int64_t wbytes = (int64_t)g.nslab * L::WST;
+  const uint32_t wslab = (uint32_t)(g.ngroup * L::WST);  // weight bytes per slab
+  const int64_t wbytes = (int64_t)g.nslab * wslab;
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)g.Wt, 0, (int)(wbytes < (int64_t)kDxInvalid ? wbytes : (int64_t)kDxInvalid), 0x00020000);
   uint32_t pbase[L::PPW];  // per piece: source byte offset of slab 0 (halo) / within a slab (weights)
@@ -214,22 +269,42 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
     const int k = (dw >= 0 && dw < IDF_DX3_DMAW) ? dw + IDF_DX3_DMAW * i : (1 << 20);
     pbase[i] = kDxInvalid;
     if (k < L::HPIECES) {
-      const int t = k / (2 * kDxPlanePieces), pl = (k / kDxPlanePieces) % 2, pi = k % kDxPlanePieces;
+      const int t = k / (2 * PLANE_KIB), pl = (k / PLANE_KIB) % 2, pi = k % PLANE_KIB;
       const int slot = 32 * pi + (lane >> 1);
-      const int tt = bid * T + t;
-      if (slot < kDxSlots && tt < g.ntiles) {
-        int q = tt;
-        const int tx = q - udiv_s(q, g.tiles_x) * g.tiles_x;
-        q = udiv_s(q, g.tiles_x);
-        const int ty = q - udiv_s(q, g.tiles_y) * g.tiles_y;
-        const int b = udiv_s(q, g.tiles_y);
-        const int hy = udiv_s(slot, kDxCW), cx = slot - hy * kDxCW;
-        const int y = 16 * ty + hy - 1, x = 16 * tx + cx - 1;
-        if (y >= 0 && y < g.H && x >= 0 && x < g.Wd)
+      const int tt = tb * T + t;
+      if (tt < g.ntiles) {
+        const DxTile dt = dx_tile(g, tt);
+        // canvas slot -> (segment, canvas row, segment column)
+        int sk, cr, cc;
+        bool ok;
+        if (g.modeb) {
+          cr = slot / PITCH;
+          const int col = slot - cr * PITCH;
+          const int b1 = dt.jc + 8;  // segment 1's first slot in a row
+          sk = (dt.jc < 16 && col >= b1) ? 1 : 0;
+          cc = col - (sk ? b1 : 0);
+          const int width = sk ? 16 - dt.jc + 2 : (dt.jc < 16 ? dt.jc : 16) + 2;
+          ok = cc < width;
+        } else {
+          sk = g.seg ? udiv_s(slot, g.seg) : 0;
+          const int rr = slot - sk * g.seg;
+          cr = rr / PITCH;
+          cc = rr - cr * PITCH;
+          ok = sk < g.nseg && cc < g.segw;
+        }
+        ok = ok && cr < g.ch;
+        const int ix = dt.ix0 + sk;
+        const int x = (sk ? 0 : dt.xf0) - 1 + cc;
+        const int vy = dt.vy0 + cr;
+        const int iy = udiv_s(vy, g.H + 2);
+        const int y = vy - iy * (g.H + 2) - 1;
+        const int b = (dt.band * g.nby + iy) * g.nbx + ix;
+        ok = ok && x >= 0 && x < g.Wd && ix < g.nbx && y >= 0 && y < g.H && iy < g.nby && b < g.B;
+        if (ok)
           pbase[i] = (uint32_t)(pl * plane_b + ((((int64_t)b * g.H + y) * g.Wd + x) * 32) + (lane & 1) * 16);
       }
     } else if (k < L::NPIECES) {
-      pbase[i] = (uint32_t)((k - L::HPIECES) * 1024 + lane * 16);
+      pbase[i] = (uint32_t)(grp * L::WST + (k - L::HPIECES) * 1024 + lane * 16);
     }
   }
   // issue piece i of slab s into stage st
@@ -244,40 +319,57 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
     int lo;
     uint32_t off;
     if (halo) {
-      const int t = k / (2 * kDxPlanePieces), pl = (k / kDxPlanePieces) % 2, pi = k % kDxPlanePieces;
-      lo = (t * 2 + pl) * kDxPlane + pi * 1024;
+      const int t = k / (2 * PLANE_KIB), pl = (k / PLANE_KIB) % 2, pi = k % PLANE_KIB;
+      lo = (t * 2 + pl) * L::PLANE + pi * 1024;
       off = pbase[i] == kDxInvalid ? kDxInvalid : pbase[i] + (uint32_t)s * xs_stride;
     } else {
       lo = L::WOFF + (k - L::HPIECES) * 1024;
-      off = pbase[i] + (uint32_t)(s * L::WST);
+      off = pbase[i] + (uint32_t)(s * g.ngroup) * (uint32_t)L::WST;  // (a product of captured
+      // locals here left the lambda's captures in scratch: 144-160 B per lane)
     }
     __builtin_amdgcn_raw_ptr_buffer_load_lds(halo ? xr : wr, (dx_lds_ptr_t)(lds + st * L::STAGE + lo),
                                              16, off, 0, 0, 0);
   };
 
   // zeros for the odd tap's pair, and the epilogue's bias table (both outside the stages)
-  // slab 0's DMA first: the bias table's dependent global loads below then overlap its latency
-  if (g.nslab > 0) {
+  // the first slab's DMA first: the bias table's dependent global loads below then overlap its
+  // latency
+  if (s1 > s0) {
 #pragma unroll
-    for (int i = 0; i < L::PPW; ++i) dma(0, 0, i);
+    for (int i = 0; i < L::PPW; ++i) dma(s0, 0, i);
   }
   for (int e = tid; e < NF * 512 / 16; e += kDxThreads) *(d4*)(lds + L::ZOFF + 16 * e) = d4{0.f, 0.f, 0.f, 0.f};
   DX3_PHASE(0, __builtin_amdgcn_s_memtime());
   DX3_PHASE(4, __builtin_amdgcn_s_memrealtime());
-  stage_bias((float*)(lds + L::BOFF), NF * 16, 0, g.N, g.b3, g.vtap, g.bfull, g.ldv, tid, kDxThreads);
+  stage_bias((float*)(lds + L::BOFF), NF * 16, grp * NF * 16, g.N, g.b3, g.vtap, g.bfull, g.ldv,
+             tid, kDxThreads);
   DX3_PHASE(1, __builtin_amdgcn_s_memtime());
 
-  // ---- fragment read offsets (bytes from a stage base).  B (pixels): lane (q = lane >> 4,
-  // j = lane & 15) reads pixel j of a halo row, 8 channels.  A (weights): output j, 8 channels.
+  // ---- the wave's canvas position: lane j's column base (its segment's base + its offset in
+  // the segment; = j mod 8) and the wave's first canvas row (its rows lie in one image)
   const int j = lane & 15, q = lane >> 4;
-  const int slot0 = r0 * kDxCW + j;
-  const int tb = tw * 2 * kDxPlane;  // the wave's tile planes
-  // [xh | xl] at (halo row r0 + h, column j + dx): q 0,1 hi plane chunk q, q 2,3 lo plane chunk q-2
-  const int oP = tb + (q >> 1) * kDxPlane + slot0 * 32 + (q & 1) * 16;
+  const DxTile dt = dx_tile(g, tile < g.ntiles ? tile : 0);
+  const int uj = dt.u0 + j;
+  const int ixj = udiv_s(uj, g.Wd);           // lane j's image column in the band
+  const int xj = uj - ixj * g.Wd;             // and its x
+  const int kj = ixj - dt.ix0;                // its segment
+  const int colb = g.modeb ? (kj ? dt.jc + 8 + (j - dt.jc) : j)
+                           : kj * g.seg + (kj ? j - (ixj * g.Wd - dt.u0) : j);
+  const int uyw = dt.u0y + r0;
+  int iyw = udiv_s(uyw, g.H);
+  if (iyw > g.nby - 1) iyw = g.nby - 1;
+  const int rowb = uyw + 2 * iyw - dt.vy0;    // canvas row of the wave's halo row 0
+
+  // ---- fragment read offsets (bytes from a stage base).  B (pixels): lane (q = lane >> 4,
+  // j = lane & 15) reads pixel j of a canvas row, 8 channels.  A (weights): output j, 8 channels.
+  const int slot0 = rowb * PITCH + colb;
+  const int tb0 = tw * 2 * L::PLANE;  // the wave's tile planes
+  // [xh | xl] at (canvas row r0 + h, column j + dx): q 0,1 hi plane chunk q, q 2,3 lo plane chunk q-2
+  const int oP = tb0 + (q >> 1) * L::PLANE + slot0 * 32 + (q & 1) * 16;
   // [xh(h, dx 0) | xh(h, dx 1)]
-  const int oF = tb + slot0 * 32 + (q & 1) * 16 + (q >> 1) * 32;
+  const int oF = tb0 + slot0 * 32 + (q & 1) * 16 + (q >> 1) * 32;
   // [xh(h, dx 2) | xh(h + 1, dx 2)]
-  const int oG = tb + slot0 * 32 + (q & 1) * 16 + 64 + (q >> 1) * kDxCW * 32;
+  const int oG = tb0 + slot0 * 32 + (q & 1) * 16 + 64 + (q >> 1) * PITCH * 32;
   // [wh(tap) ; wh(tap)] at tap t, fragment n: + (t * NF + n) * 512
   const int oAH = L::WOFF + j * 32 + (q & 1) * 16;
   // [wl(dy, 0) ; wl(dy, 1)]: + (3 dy * NF + n) * 512
@@ -315,17 +407,17 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   //   steps [4 HR, NS)    (G, h = t - 4 HR):            [wl(0,2) ; wl(1,2)] and [0 ; wl(2,2)]
   //                                                      . [xh(h,2) | xh(h+1,2)]
   // Pixel fragments are read DB steps ahead (a ring of DB + 1), a phase's weight fragments in
-  // the first three steps of the phase before it.  Two LDS stages: slab s reads stage s % 2; after the slab's
-  // barrier (every wave's DMA of slab s landed, every wave done with slab s - 1) the waves DMA
-  // slab s + 1 into the other stage, one piece per step.
+  // the first three steps of the phase before it.  Two LDS stages: slab s reads stage
+  // (s - s0) % 2; after the slab's barrier (every wave's DMA of slab s landed, every wave done
+  // with slab s - 1) the waves DMA slab s + 1 into the other stage, one piece per step.
   constexpr int DB = IDF_DX3_DB, RB = DB + 1;
   e8 Bq[RB];
   e8 AS[2][3][NF];  // weight sets: P0 / P2 in 0, P1 / F in 1
   e8 AZ[2][NF];     // G: [wl(0,2) ; wl(1,2)] and [0 ; wl(2,2)]
   auto read_B = [&](const char* st, int t) -> e8 {
-    if (t < 3 * HR) return rdB(st + oP + ((t % HR) * kDxCW + t / HR) * 32);
-    if (t < 4 * HR) return rdB(st + oF + (t - 3 * HR) * kDxCW * 32);
-    return rdB(st + oG + (t - 4 * HR) * kDxCW * 32);
+    if (t < 3 * HR) return rdB(st + oP + ((t % HR) * PITCH + t / HR) * 32);
+    if (t < 4 * HR) return rdB(st + oF + (t - 3 * HR) * PITCH * 32);
+    return rdB(st + oG + (t - 4 * HR) * PITCH * 32);
   };
   // weight fragments of phase p (0-2: P dx = p, 3: F), kernel row dy
   auto read_A = [&](const char* st, int p, int dy, e8 (&A)[NF]) {
@@ -344,186 +436,142 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
     }
   };
 
-  const int nslab = g.nslab;
-  if constexpr (IDF_DX3_XPF) {
-    constexpr int X = (IDF_DX3_X < NS - DB && IDF_DX3_X + 1 >= 3 * HR) ? IDF_DX3_X : NS - DB - 3;
-    static_assert(X + 1 >= 3 * HR && NS - DB > X && X >= L::PPW, "cross-slab prefetch schedule");
-    if (nslab > 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (nslab > 1) {
+  for (int s = s0; s < s1; ++s) {
+    const char* cur = lds + ((s - s0) & 1) * L::STAGE;
+    // this wave's DMA of slab s landed; after the barrier every wave's has, and every wave is
+    // done reading the other stage (slab s - 1)
+    DX3_STAMP(s - s0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!(IDF_DX3_ABLATE & 8)) __builtin_amdgcn_s_barrier();
+    DX3_STAMP(s - s0, 1);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int i = 0; i < L::PPW; ++i) dma(1, 1, i);
-      }
+    for (int dy = 0; dy < 3; ++dy) read_A(cur, 0, dy, AS[0][dy]);
 #pragma unroll
-      for (int dy = 0; dy < 3; ++dy) read_A(lds, 0, dy, AS[0][dy]);
-#pragma unroll
-      for (int k = 0; k < DB; ++k) Bq[k] = read_B(lds, k);
-    }
-    for (int s = 0; s < nslab; ++s) {
-      const char* cur = lds + (s & 1) * L::STAGE;
-      const char* nxt = lds + ((s + 1) & 1) * L::STAGE;
-      const bool more = s + 1 < nslab;
-      DX3_STAMP(s, 0);
-      // every wave is done with slab s - 1: its stage may take slab s + 1
-      if (s >= 1) __builtin_amdgcn_s_barrier();
-      DX3_STAMP(s, 1);
-      auto step = [&](auto tc) {
-        constexpr int t = decltype(tc)::value;
-        if (IDF_DX3_SB) __builtin_amdgcn_sched_barrier(0);
-        if constexpr (t == 9) DX3_STAMP(s, 2);
-        if constexpr (t < L::PPW) {
-          if (s >= 1 && more) dma(s + 1, (s + 1) & 1, t);
-        }
-        if constexpr (t == X) {  // slab s + 1's stage complete (every wave's DMA landed)
+    for (int k = 0; k < DB; ++k) Bq[k] = read_B(cur, k);
+    const bool more = s + 1 < s1;
+    const int nst = (s + 1 - s0) & 1;
+    auto step = [&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      if (IDF_DX3_SB) __builtin_amdgcn_sched_barrier(0);  // keep the schedule: steps do not mix
+      if constexpr (t == 9) DX3_STAMP(s - s0, 2);
+      // slab s + 1's DMA, one piece every IDF_DX3_DMAS steps from step IDF_DX3_DMA0
+      constexpr int ds = IDF_DX3_DMAS > 0 ? IDF_DX3_DMAS : 1;
+      auto dma_at = [&](auto dtc) {
+        constexpr int dt_ = decltype(dtc)::value;
+        if constexpr (IDF_DX3_DMAS == 0 && dt_ == 0) {  // the whole slab's pieces at once
           if (more) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-          }
-        }
-        if constexpr (t < 3) read_A(cur, 1, t, AS[1][t]);
-        if constexpr (t >= HR && t < HR + 3) read_A(cur, 2, t - HR, AS[0][t - HR]);
-        if constexpr (t >= 2 * HR && t < 2 * HR + 3) read_A(cur, 3, t - 2 * HR, AS[1][t - 2 * HR]);
-        if constexpr (t == 2 * HR + 3 || t == 2 * HR + 4) {
 #pragma unroll
-          for (int n = 0; n < NF; ++n) {
-            if (t == 2 * HR + 3) AZ[0][n] = rdA(cur + oAG + n * 512);
-            else AZ[1][n] = rdA(zlane ? zO + n * 512 : cur + oAO + n * 512);
+            for (int i = 0; i < L::PPW; ++i) dma(s + 1, nst, i);
           }
-        }
-        // slab s + 1's first weights (AS[0] is free once phase 2 is done)
-        if constexpr (t > X && t <= X + 3) {
-          if (more) read_A(nxt, 0, t - X - 1, AS[0][t - X - 1]);
-        }
-        if constexpr (t + DB < NS) Bq[(t + DB) % RB] = read_B(cur, t + DB);
-        else if (more) Bq[(t + DB) % RB] = read_B(nxt, t + DB - NS);
-        const e8& Bv = Bq[t % RB];
-        if constexpr (t < 3 * HR) {
-          mma_rows(AS[(t / HR) & 1], Bv, t % HR);
-        } else if constexpr (t < 4 * HR) {
-          mma_rows(AS[1], Bv, t - 3 * HR);
-        } else {
-          constexpr int h = t - 4 * HR;
-          if constexpr (h < WR) {
-#pragma unroll
-            for (int n = 0; n < NF; ++n) mma(AZ[0][n], Bv, acc[h][n]);
-          }
-          if constexpr (h > 0) {
-#pragma unroll
-            for (int n = 0; n < NF; ++n) mma(AZ[1][n], Bv, acc[h - 1][n]);
-          }
+        } else if constexpr (IDF_DX3_DMAS > 0 && dt_ >= 0 && dt_ % ds == 0 && dt_ / ds < L::PPW) {
+          if (more) dma(s + 1, nst, dt_ / ds);
         }
       };
-      dx_unroll(step, std::make_integer_sequence<int, NS>{});
-      DX3_STAMP(s, 3);
-      // the ring ran NS steps: slab s + 1's fragment k is in Bq[(NS + k) % RB]
-      e8 f[DB];
+      if (IDF_DX3_STAG == 0 || !(wave & 4)) dma_at(std::integral_constant<int, t - IDF_DX3_DMA0>{});
+      else dma_at(std::integral_constant<int, t - IDF_DX3_DMA0 - IDF_DX3_STAG>{});
+      // weights of the next phase, one kernel row per step, in the first three steps of the
+      // phase before it (its register set was freed by the phase before that)
+      if constexpr (t < 3) read_A(cur, 1, t, AS[1][t]);
+      if constexpr (t >= HR && t < HR + 3) read_A(cur, 2, t - HR, AS[0][t - HR]);
+      if constexpr (t >= 2 * HR && t < 2 * HR + 3) read_A(cur, 3, t - 2 * HR, AS[1][t - 2 * HR]);
+      if constexpr (t == 2 * HR + 3 || t == 2 * HR + 4) {
 #pragma unroll
-      for (int k = 0; k < DB; ++k) f[k] = Bq[(NS + k) % RB];
-#pragma unroll
-      for (int k = 0; k < DB; ++k) Bq[k] = f[k];
-    }
-  } else {
-    const int nslab = g.nslab;
-    for (int s = 0; s < nslab; ++s) {
-      const char* cur = lds + (s & 1) * L::STAGE;
-      // this wave's DMA of slab s landed; after the barrier every wave's has, and every wave is
-      // done reading stage (s + 1) % 2 (slab s - 1)
-      DX3_STAMP(s, 0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (!(IDF_DX3_ABLATE & 8)) __builtin_amdgcn_s_barrier();
-      DX3_STAMP(s, 1);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int dy = 0; dy < 3; ++dy) read_A(cur, 0, dy, AS[0][dy]);
-#pragma unroll
-      for (int k = 0; k < DB; ++k) Bq[k] = read_B(cur, k);
-      const bool more = s + 1 < nslab;
-      auto step = [&](auto tc) {
-        constexpr int t = decltype(tc)::value;
-        if (IDF_DX3_SB) __builtin_amdgcn_sched_barrier(0);  // keep the schedule: steps do not mix
-        if constexpr (t == 9) DX3_STAMP(s, 2);
-        // slab s + 1's DMA, one piece every IDF_DX3_DMAS steps from step IDF_DX3_DMA0
-        constexpr int ds = IDF_DX3_DMAS > 0 ? IDF_DX3_DMAS : 1;
-        auto dma_at = [&](auto dtc) {
-          constexpr int dt = decltype(dtc)::value;
-          if constexpr (IDF_DX3_DMAS == 0 && dt == 0) {  // the whole slab's pieces at once
-            if (more) {
-#pragma unroll
-              for (int i = 0; i < L::PPW; ++i) dma(s + 1, (s + 1) & 1, i);
-            }
-          } else if constexpr (IDF_DX3_DMAS > 0 && dt >= 0 && dt % ds == 0 && dt / ds < L::PPW) {
-            if (more) dma(s + 1, (s + 1) & 1, dt / ds);
-          }
-        };
-        if (IDF_DX3_STAG == 0 || !(wave & 4)) dma_at(std::integral_constant<int, t - IDF_DX3_DMA0>{});
-        else dma_at(std::integral_constant<int, t - IDF_DX3_DMA0 - IDF_DX3_STAG>{});
-        // weights of the next phase, one kernel row per step, in the first three steps of the
-        // phase before it (its register set was freed by the phase before that)
-        if constexpr (t < 3) read_A(cur, 1, t, AS[1][t]);
-        if constexpr (t >= HR && t < HR + 3) read_A(cur, 2, t - HR, AS[0][t - HR]);
-        if constexpr (t >= 2 * HR && t < 2 * HR + 3) read_A(cur, 3, t - 2 * HR, AS[1][t - 2 * HR]);
-        if constexpr (t == 2 * HR + 3 || t == 2 * HR + 4) {
-#pragma unroll
-          for (int n = 0; n < NF; ++n) {
-            if (t == 2 * HR + 3) AZ[0][n] = rdA(cur + oAG + n * 512);
-            else AZ[1][n] = rdA(zlane ? zO + n * 512 : cur + oAO + n * 512);
-          }
+        for (int n = 0; n < NF; ++n) {
+          if (t == 2 * HR + 3) AZ[0][n] = rdA(cur + oAG + n * 512);
+          else AZ[1][n] = rdA(zlane ? zO + n * 512 : cur + oAO + n * 512);
         }
-        // pixel fragment DB steps ahead (within the slab)
-        if constexpr (t + DB < NS) Bq[(t + DB) % RB] = read_B(cur, t + DB);
-        const e8& Bv = Bq[t % RB];
-        if constexpr (t < 3 * HR) {
-          mma_rows(AS[(t / HR) & 1], Bv, t % HR);
-        } else if constexpr (t < 4 * HR) {
-          mma_rows(AS[1], Bv, t - 3 * HR);
-        } else {
-          constexpr int h = t - 4 * HR;
-          if constexpr (h < WR) {
+      }
+      // pixel fragment DB steps ahead (within the slab)
+      if constexpr (t + DB < NS) Bq[(t + DB) % RB] = read_B(cur, t + DB);
+      const e8& Bv = Bq[t % RB];
+      if constexpr (t < 3 * HR) {
+        mma_rows(AS[(t / HR) & 1], Bv, t % HR);
+      } else if constexpr (t < 4 * HR) {
+        mma_rows(AS[1], Bv, t - 3 * HR);
+      } else {
+        constexpr int h = t - 4 * HR;
+        if constexpr (h < WR) {
 #pragma unroll
-            for (int n = 0; n < NF; ++n) mma(AZ[0][n], Bv, acc[h][n]);
-          }
-          if constexpr (h > 0) {
-#pragma unroll
-            for (int n = 0; n < NF; ++n) mma(AZ[1][n], Bv, acc[h - 1][n]);
-          }
+          for (int n = 0; n < NF; ++n) mma(AZ[0][n], Bv, acc[h][n]);
         }
-      };
-      dx_unroll(step, std::make_integer_sequence<int, NS>{});
-      DX3_STAMP(s, 3);
+        if constexpr (h > 0) {
+#pragma unroll
+          for (int n = 0; n < NF; ++n) mma(AZ[1][n], Bv, acc[h - 1][n]);
+        }
+      }
+    };
+    dx_unroll(step, std::make_integer_sequence<int, NS>{});
+    DX3_STAMP(s - s0, 3);
+  }
+  DX3_PHASE(2, __builtin_amdgcn_s_memtime());
+
+  // ---- split K: every chunk's block stores its raw sums; the tile's last block to finish
+  // adds them in chunk order (its own from registers -- the same bits) and runs the epilogue
+  if (g.nchunk > 1) {
+    constexpr int FR = kDxWaves * WR * NF;  // fragments per block
+    const int64_t pb = ((int64_t)(tb * g.ngroup + grp) * g.nchunk) * FR * 64;  // d4 index of chunk 0
+    d4* part = (d4*)g.part;
+#pragma unroll
+    for (int m = 0; m < WR; ++m)
+#pragma unroll
+      for (int n = 0; n < NF; ++n)
+        part[pb + ((int64_t)chunk * FR + (wave * WR + m) * NF + n) * 64 + lane] = acc[m][n];
+    __threadfence();  // release: this wave's partials visible at agent scope
+    __syncthreads();
+    if (tid == 0) {
+      // wraps to 0 at the last arrival: the counter is zero again for the next launch
+      const uint32_t old = __builtin_amdgcn_atomic_inc32(g.ctr + tb * g.ngroup + grp,
+                                                         (uint32_t)(g.nchunk - 1), __ATOMIC_ACQ_REL,
+                                                         "agent");
+      *last_flag = old == (uint32_t)(g.nchunk - 1);
     }
+    __syncthreads();
+    if (!*last_flag) return;
+    __threadfence();  // acquire: the other chunks' partials
+#pragma unroll
+    for (int m = 0; m < WR; ++m)
+#pragma unroll
+      for (int n = 0; n < NF; ++n) {
+        d4 sum = chunk == 0 ? acc[m][n] : part[pb + ((int64_t)(wave * WR + m) * NF + n) * 64 + lane];
+        for (int c = 1; c < g.nchunk; ++c) {
+          const d4 v = c == chunk ? acc[m][n]
+                                  : part[pb + ((int64_t)c * FR + (wave * WR + m) * NF + n) * 64 + lane];
+          sum = sum + v;
+        }
+        acc[m][n] = sum;
+      }
   }
 
-  // ---- epilogue: lane holds outputs 16n + 4q .. +3 of pixel (row r0 + m, column j) of its
-  // tile.  fp32 outputs to out; their split pairs to XS at channel C + 16n + 4q (zeros for the
-  // padding outputs n >= N and on to the next 16-channel boundary past C + N, so the next
-  // layer's last slab reads finite values; never past the split buffer).
-  DX3_PHASE(2, __builtin_amdgcn_s_memtime());
+  // ---- epilogue: lane holds outputs 16 (grp NF + n) + 4q .. +3 of packed pixel (row r0 + m,
+  // column j) of its tile.  fp32 outputs to out; their split pairs to XS at channel C + that
+  // output (zeros for the padding outputs >= N and -- the last group -- on to the next
+  // 16-channel boundary past C + N, so the next layer's last slab reads finite values; never
+  // past the split buffer).
   if (tile >= g.ntiles) return;
-  int qt = tile;
-  const int tx = qt - udiv_s(qt, g.tiles_x) * g.tiles_x;
-  qt = udiv_s(qt, g.tiles_x);
-  const int ty = qt - udiv_s(qt, g.tiles_y) * g.tiles_y;
-  const int b = udiv_s(qt, g.tiles_y);
+  const int b_img = (dt.band * g.nby + iyw) * g.nbx + ixj;
+  if (b_img >= g.B) return;
   const WAct act(g.act, g.slope);
   const float* btab = (const float*)(lds + L::BOFF);
   bool out_ok = true;
-  const int x = 16 * tx + j;
   const int zr = (g.C + g.N + 15) / 16 * 16, zend = zr < 16 * g.nslab_xs ? zr : 16 * g.nslab_xs;
+  const bool lastg = grp == g.ngroup - 1;
   char* xsb = (char*)g.xs;
 #pragma unroll
   for (int m = 0; m < WR; ++m) {
-    const int y = 16 * ty + r0 + m;
-    if (y >= g.H || x >= g.Wd) continue;
-    const int cls = bias_class(y, x, g.H, g.Wd);
-    const int64_t pix = ((int64_t)b * g.H + y) * g.Wd + x;
+    const int y = uyw + m - iyw * g.H;
+    if (y >= g.H) continue;
+    const int cls = bias_class(y, xj, g.H, g.Wd);
+    const int64_t pix = ((int64_t)b_img * g.H + y) * g.Wd + xj;
     float* dst = g.out + pix * g.ldo;
 #pragma unroll
     for (int n = 0; n <= NF; ++n) {
-      const int n0 = 16 * n + 4 * q;
+      if (n == NF && !lastg) break;
+      const int nl = 16 * n + 4 * q;              // within the group
+      const int n0 = 16 * grp * NF + nl;          // output column
       d4 v = d4{0.f, 0.f, 0.f, 0.f};
       if (n < NF && n0 < g.N) {
-        const d4 bv = *(const d4*)(btab + cls * (NF * 16) + n0);
+        const d4 bv = *(const d4*)(btab + cls * (NF * 16) + nl);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const float t = acc[m][n][k] * g.yscale + bv[k];
@@ -562,13 +610,17 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
 // finite (these zeros, and outputs under the |y| < 8192 guard), so the product is +-0 either
 // way and the sum's bits do not depend on which value was read);
 // ORs bit 0 of flag for a value that is NaN or |x| >= 32768 (the f16 pairs' range).  One
-// thread per (pixel, 4 channels).
+// thread per (pixel, 4 channels).  Threads [0, nzero) also clear zero[] (the split-K tile
+// counters of the block's dx3 layers, idf_conv3x3_dx3: zero before a block's first layer).
 __global__ void __launch_bounds__(256) dx3_split_cols_kernel(int64_t P, int32_t c0, int32_t c1,
                                                              const float* __restrict__ x,
                                                              int64_t ld_x, uint16_t* __restrict__ xs,
-                                                             uint32_t* __restrict__ flag) {
+                                                             uint32_t* __restrict__ flag,
+                                                             uint32_t* __restrict__ zero,
+                                                             int32_t nzero) {
   const int nq = ((c1 + 15) / 16 * 16 - c0) / 4;  // channel quads per pixel
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < nzero) zero[g] = 0u;
   if (g >= P * nq) return;
   const int64_t pix = g / nq;
   const int c = c0 + 4 * (int)(g - pix * nq);
@@ -585,6 +637,58 @@ __global__ void __launch_bounds__(256) dx3_split_cols_kernel(int64_t P, int32_t 
   if (!ok && flag) atomicOr(flag, 1u);
 }
 
+// ---- geometry plan (host): how a (H, W, N) layer tiles, packs and splits.  A function of the
+// image geometry, the output count and C only -- never of the batch -- so an encoder and its
+// decoder run every layer with the same tiles, chunks and summation order.
+#ifndef IDF_DX3_KSPLIT
+#define IDF_DX3_KSPLIT 4  // chunks of the split-K levels (timing A/B builds only: changes bits)
+#endif
+struct Dx3Plan {
+  int ok, pitch, plane_kib, nbx, nby, ch, seg, segw, nseg, modeb, nf, ngroup, split;
+};
+
+static int dx3_gcd(int a, int b) { return b ? dx3_gcd(b, a % b) : a; }
+
+static Dx3Plan dx3_plan(int H, int W, int N) {
+  Dx3Plan p = {};
+  if (H < 1 || W < 1 || N < 1 || N > 1024) return p;
+  const int nft = (N + 15) / 16;
+  p.nf = nft <= 4 ? nft : 4;
+  p.ngroup = (nft + p.nf - 1) / p.nf;
+  if (W % 16 == 0) {  // 16-wide tiles of one image, any H
+    p.nbx = 1; p.pitch = 18; p.segw = 18; p.nseg = 1; p.plane_kib = 11;
+  } else if (W == 4 || W == 8) {  // 16 / W images across a tile, one segment each
+    p.nbx = 16 / W; p.pitch = W + 2; p.segw = W + 2; p.nseg = p.nbx;
+    p.plane_kib = W == 8 ? 13 : 19;
+  } else if (W > 16) {  // bands of nbx images (a multiple of 16 wide): <= one edge per tile
+    p.nbx = 16 / dx3_gcd(W, 16); p.pitch = 26; p.modeb = 1; p.nseg = 2; p.plane_kib = 17;
+  } else {
+    return p;
+  }
+  if (p.nbx > 1 && (H == 2 || H == 4 || H == 8)) {  // images stacked down a tile, gutter rows
+    p.nby = 16 / H;
+    p.ch = p.nby * (H + 2);
+  } else {
+    p.nby = 1;
+    p.ch = 18;
+  }
+  int slots = p.ch * p.pitch;
+  if (!p.modeb && p.nseg > 1) {
+    // segment stride = W (mod 8) slots: lane j's column base is then j (mod 8) in every
+    // segment, so the fragment reads stay bank-conflict-free
+    int s = p.ch * p.pitch;
+    while ((s - W) % 8) ++s;
+    p.seg = s;
+    slots = p.nseg * s;
+  }
+  if ((slots * 32 + 1023) / 1024 > p.plane_kib) return p;
+  // split K where a level's tiles are few for any batch the bench runs (imagenet64's 8 x 8:
+  // 64 tiles per 256 images): by the geometry alone
+  p.split = (H * W <= 64 && p.nbx * p.nby <= 4) ? IDF_DX3_KSPLIT : 1;
+  p.ok = 1;
+  return p;
+}
+
 }  // namespace idf
 
 using namespace idf;
@@ -596,8 +700,46 @@ extern "C" int idf_dx3_stamps(unsigned long long* host) {
 }
 #endif
 
+namespace {
+
+struct Dx3Launch {
+  Dx3Plan pl;
+  int64_t ntiles;
+  int T, nblk_tiles, nslab, nchunk, chunk_slabs;
+  int64_t ctr_bytes, part_bytes;
+};
+
+// the launch shape of a layer: tiles, tiles per block (two where every CU still gets a block,
+// at the 16-wide canvas), split-K chunks and the workspace they need
+Dx3Launch dx3_launch_shape(int B, int H, int W, int C, int N) {
+  Dx3Launch s = {};
+  s.pl = dx3_plan(H, W, N);
+  if (!s.pl.ok || B < 1) return s;
+  const int64_t nbands = (B + s.pl.nbx * s.pl.nby - 1) / (s.pl.nbx * s.pl.nby);
+  const int tiles_x = s.pl.nbx * W / 16, tiles_y = (s.pl.nby * H + 15) / 16;
+  s.ntiles = nbands * tiles_x * tiles_y;
+  s.nslab = (C + 15) / 16;
+  s.chunk_slabs = s.nslab > 0 ? (s.nslab + s.pl.split - 1) / s.pl.split : 1;
+  s.nchunk = s.nslab > 0 ? (s.nslab + s.chunk_slabs - 1) / s.chunk_slabs : 1;
+  const bool two = s.pl.pitch == 18 && s.pl.nf <= 3 && s.nchunk == 1 && s.ntiles >= 2 * 256 &&
+                   !IDF_DX3_FORCE1;
+  s.T = two ? 2 : 1;  // two tiles (4 rows per wave) or one (2 rows)
+  s.nblk_tiles = (int)((s.ntiles + s.T - 1) / s.T);
+  if (s.nchunk > 1) {
+    const int64_t fr = (int64_t)kDxWaves * (16 / kDxWaves) * s.pl.nf;  // fragments per block
+    s.ctr_bytes = ((int64_t)s.nblk_tiles * s.pl.ngroup * 4 + 255) / 256 * 256;
+    // room for the most chunks any C up to this one splits into (nchunk is not monotonic in
+    // C: 7 slabs make 4 chunks of 2, 9 slabs 3 of 3), so one workspace serves a block's layers
+    const int most = s.nslab < s.pl.split ? s.nslab : s.pl.split;
+    s.part_bytes = (int64_t)s.nblk_tiles * s.pl.ngroup * most * fr * 64 * 16;
+  }
+  return s;
+}
+
+}  // namespace
+
 extern "C" int idf_conv3x3_dx3_supported(int32_t H, int32_t W, int32_t N) {
-  return H >= 1 && W >= 16 && W % 16 == 0 && N >= 1 && N <= 48;
+  return dx3_plan(H, W, N).ok;
 }
 
 extern "C" int64_t idf_dx3_split_bytes(int64_t P, int32_t channels) {
@@ -605,14 +747,35 @@ extern "C" int64_t idf_dx3_split_bytes(int64_t P, int32_t channels) {
   return (int64_t)((channels + 15) / 16) * 2 * P * 32;
 }
 
+extern "C" int64_t idf_conv3x3_dx3_counter_bytes(int32_t B, int32_t H, int32_t W, int32_t N) {
+  const Dx3Launch s = dx3_launch_shape(B, H, W, 16 * 64, N);  // the widest split: every chunk count
+  if (!s.pl.ok) return -1;
+  if (s.pl.split <= 1) return 0;
+  return ((int64_t)s.nblk_tiles * s.pl.ngroup * 4 + 255) / 256 * 256;
+}
+
+extern "C" int64_t idf_conv3x3_dx3_workspace(int32_t B, int32_t H, int32_t W, int32_t C, int32_t N) {
+  const Dx3Launch s = dx3_launch_shape(B, H, W, C, N);
+  if (!s.pl.ok) return -1;
+  if (s.nchunk <= 1) return 0;
+  return idf_conv3x3_dx3_counter_bytes(B, H, W, N) + s.part_bytes;
+}
+
 extern "C" int idf_dx3_split_cols(void* stream, int64_t P, int32_t c0, int32_t c1, const float* x,
-                                  int64_t ld_x, uint16_t* xs, int32_t nslab_xs, uint32_t* d_flag) {
-  if (P <= 0 || c1 <= c0) return (P < 0 || c1 < c0) ? IDF_ERR_ARG : IDF_OK;
+                                  int64_t ld_x, uint16_t* xs, int32_t nslab_xs, uint32_t* d_flag,
+                                  uint32_t* d_zero, int32_t nzero) {
+  if (P < 0 || c1 < c0 || nzero < 0 || (nzero && !d_zero)) return IDF_ERR_ARG;
+  if (P == 0 || c1 == c0) {
+    if (nzero) return hipMemsetAsync(d_zero, 0, 4 * (size_t)nzero, (hipStream_t)stream) == hipSuccess
+                          ? IDF_OK : IDF_ERR_HIP;
+    return IDF_OK;
+  }
   if (!x || !xs || (c0 & 15) || (c1 & 3) || (ld_x & 3) || (uintptr_t)x % 16) return IDF_ERR_ARG;
   if ((c1 + 15) / 16 > nslab_xs) return IDF_ERR_ARG;
-  const int64_t n = P * (((c1 + 15) / 16 * 16 - c0) / 4);
+  int64_t n = P * (((c1 + 15) / 16 * 16 - c0) / 4);
+  if (n < nzero) n = nzero;
   hipLaunchKernelGGL(dx3_split_cols_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, P, c0, c1, x, ld_x, xs, d_flag);
+                     (hipStream_t)stream, P, c0, c1, x, ld_x, xs, d_flag, d_zero, nzero);
   return idf_last_error();
 }
 
@@ -620,42 +783,70 @@ extern "C" int idf_conv3x3_dx3(void* stream, int32_t B, int32_t H, int32_t W, in
                                uint16_t* xs, int32_t nslab_xs, const uint16_t* w, int32_t nft,
                                float yscale, const float* b3, const float* vtap, int32_t ldv,
                                const float* bfull, int32_t N, float* out, int64_t ld_out,
-                               int32_t act, float slope, uint32_t* d_flag) {
+                               int32_t act, float slope, uint32_t* d_flag, void* d_workspace,
+                               int64_t workspace_bytes) {
   if (B <= 0 || H <= 0 || W <= 0 || N <= 0) return IDF_OK;
   if (C <= 0 || (C & 3) || !w || !xs || !out || !b3) return IDF_ERR_ARG;
-  if (!idf_conv3x3_dx3_supported(H, W, N)) return IDF_ERR_UNSUPPORTED;
-  const int nf = (N + 15) / 16;
-  if (nft != nf) return IDF_ERR_ARG;  // the weights hold exactly the kernel's fragments
+  const Dx3Launch sh = dx3_launch_shape(B, H, W, C, N);
+  if (!sh.pl.ok) return IDF_ERR_UNSUPPORTED;
+  // the weights hold exactly the kernel's fragments: ngroup groups of nf, nft = ngroup * nf
+  if (nft != sh.pl.ngroup * sh.pl.nf) return IDF_ERR_ARG;
   if (vtap && (!bfull || ldv < N)) return IDF_ERR_ARG;
   if ((uintptr_t)out % 16 || ld_out % 4) return IDF_ERR_ARG;  // 16-B output stores
   if ((C + 15) / 16 > nslab_xs) return IDF_ERR_ARG;          // the input slabs must exist
   const int64_t P = (int64_t)B * H * W;
   // 32-bit buffer offsets: the split buffer must span < 4 GiB
   if (idf_dx3_split_bytes(P, 16 * nslab_xs) >= (int64_t)kDxInvalid) return IDF_ERR_UNSUPPORTED;
+  const int64_t nblk = (int64_t)sh.nblk_tiles * sh.pl.ngroup * sh.nchunk;
+  if (sh.ntiles >= (1 << 20) || nblk >= (1 << 20)) return IDF_ERR_UNSUPPORTED;  // udiv_s operands
   Dx3Args g = {};
+  if (sh.nchunk > 1) {
+    const int64_t cb = idf_conv3x3_dx3_counter_bytes(B, H, W, N);
+    if (!d_workspace || (uintptr_t)d_workspace % 256 || workspace_bytes < cb + sh.part_bytes)
+      return IDF_ERR_WORKSPACE;
+    g.ctr = (uint32_t*)d_workspace;
+    g.part = (float*)((char*)d_workspace + cb);
+  }
   g.xs = xs; g.P = P; g.nslab_xs = nslab_xs; g.C = C;
-  g.Wt = w; g.nslab = (C + 15) / 16; g.nft = nft; g.N = N;
+  g.Wt = w; g.nslab = sh.nslab; g.ngroup = sh.pl.ngroup; g.N = N;
   g.B = B; g.H = H; g.Wd = W;
-  g.tiles_y = (H + 15) / 16;
-  g.tiles_x = W / 16;
-  const int64_t ntiles = (int64_t)B * g.tiles_y * g.tiles_x;
-  if (ntiles >= (1 << 20)) return IDF_ERR_UNSUPPORTED;  // udiv_s operands
-  g.ntiles = (int32_t)ntiles;
+  g.nbx = sh.pl.nbx; g.nby = sh.pl.nby;
+  g.tiles_x = sh.pl.nbx * W / 16;
+  g.tiles_y = (sh.pl.nby * H + 15) / 16;
+  g.ntiles = (int32_t)sh.ntiles;
+  g.nblk_tiles = sh.nblk_tiles;
+  g.ch = sh.pl.ch; g.seg = sh.pl.seg; g.segw = sh.pl.segw; g.nseg = sh.pl.nseg; g.modeb = sh.pl.modeb;
+  g.nchunk = sh.nchunk; g.chunk_slabs = sh.chunk_slabs;
   g.b3 = b3; g.vtap = vtap; g.bfull = bfull; g.ldv = ldv; g.act = act; g.slope = slope;
   g.out = out; g.ldo = ld_out; g.yscale = yscale; g.flag = d_flag;
   hipStream_t s = (hipStream_t)stream;
-  // two tiles per block (4 rows per wave) while that still gives every CU a block; else one
-  // tile per block (2 rows per wave)
-  const bool two = ntiles >= 2 * 256 && !IDF_DX3_FORCE1;
-#define IDF_DX3_LAUNCH(nf_, wr_)                                                                   \
-  hipLaunchKernelGGL((conv3_dx3_kernel<nf_, wr_>),                                               \
-                     dim3((unsigned)((ntiles + Dx3Lds<nf_, wr_>::T - 1) / Dx3Lds<nf_, wr_>::T)), \
-                     dim3(kDxThreads), 0, s, g)
-  switch (nf) {
-    case 1: if (two) IDF_DX3_LAUNCH(1, 32 / kDxWaves); else IDF_DX3_LAUNCH(1, 16 / kDxWaves); break;
-    case 2: if (two) IDF_DX3_LAUNCH(2, 32 / kDxWaves); else IDF_DX3_LAUNCH(2, 16 / kDxWaves); break;
-    default: if (two) IDF_DX3_LAUNCH(3, 32 / kDxWaves); else IDF_DX3_LAUNCH(3, 16 / kDxWaves); break;
+  const dim3 grid((unsigned)nblk), blk(kDxThreads);
+#define IDF_DX3_GO(nf_, wr_, pitch_, kib_) \
+  hipLaunchKernelGGL((conv3_dx3_kernel<nf_, wr_, pitch_, kib_>), grid, blk, 0, s, g)
+#define IDF_DX3_NF(wr_, pitch_, kib_)                      \
+  switch (sh.pl.nf) {                                      \
+    case 1: IDF_DX3_GO(1, wr_, pitch_, kib_); break;       \
+    case 2: IDF_DX3_GO(2, wr_, pitch_, kib_); break;       \
+    case 3: IDF_DX3_GO(3, wr_, pitch_, kib_); break;       \
+    default: IDF_DX3_GO(4, wr_, pitch_, kib_); break;      \
   }
-#undef IDF_DX3_LAUNCH
+  constexpr int W2 = 16 / kDxWaves, W4 = 32 / kDxWaves;  // rows per wave: one tile / two tiles
+  if (sh.T == 2) {
+    switch (sh.pl.nf) {
+      case 1: IDF_DX3_GO(1, W4, 18, 11); break;
+      case 2: IDF_DX3_GO(2, W4, 18, 11); break;
+      default: IDF_DX3_GO(3, W4, 18, 11); break;
+    }
+  } else if (sh.pl.pitch == 18) {
+    IDF_DX3_NF(W2, 18, 11)
+  } else if (sh.pl.pitch == 10) {
+    IDF_DX3_NF(W2, 10, 13)
+  } else if (sh.pl.pitch == 6) {
+    IDF_DX3_NF(W2, 6, 19)
+  } else {
+    IDF_DX3_NF(W2, 26, 17)
+  }
+#undef IDF_DX3_NF
+#undef IDF_DX3_GO
   return idf_last_error();
 }

@@ -637,12 +637,28 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
   dx3 = dx3 && n_dx3 > 0;
   uint16_t* xs = nullptr;
   int32_t nslab_xs = 0;
+  char* dws = nullptr;  // the dx3 layers' split-K counters and partial sums, after the copy
+  int64_t dws_bytes = 0;
+  const int dx3_nft = [&] {  // fragments the dx3 weights hold (packing.dx3_groups)
+    const int nft = (blk->g_pad + 15) / 16, nf = nft < 4 ? nft : 4;
+    return (nft + nf - 1) / nf * nf;
+  }();
   if (dx3) {
-    nslab_xs = (int32_t)std::min<int64_t>(ld_tmp / 16, ((int64_t)blk->k_in[blk->depth] + 15) / 16);
-    if (nslab_xs < (blk->k_in[n_dx3 - 1] + 15) / 16) return IDF_ERR_WORKSPACE;
+    // the slabs the dx3 layers read: up to the last one's input (its own outputs are read by
+    // no dx3 layer, so they are split only into the slab it reads)
+    nslab_xs = (blk->k_in[n_dx3 - 1] + 15) / 16;
+    const int64_t xs_bytes = idf_dx3_split_bytes(P, 16 * nslab_xs);
+    const int64_t avail = ws_floats * 4;
+    const int64_t off = (xs_bytes + 255) / 256 * 256;
+    const int64_t need = idf_conv3x3_dx3_workspace(B, H, W, blk->k_in[n_dx3 - 1], blk->g_pad);
+    if (need < 0 || off + need > avail || (uintptr_t)tmp % 256) return IDF_ERR_WORKSPACE;
     xs = (uint16_t*)tmp;
+    dws = (char*)tmp + off;
+    dws_bytes = avail - off;
+    const int64_t ctr = idf_conv3x3_dx3_counter_bytes(B, H, W, blk->g_pad);
     int rc = idf_dx3_split_cols(stream, P, 0, blk->k_in[0], feat, ld_feat, xs, nslab_xs,
-                                blk->range_flag);
+                                blk->range_flag, need > 0 ? (uint32_t*)dws : nullptr,
+                                need > 0 ? (int32_t)(ctr / 4) : 0);
     if (rc) return rc;
   }
   for (int i = 0; i < blk->depth; ++i) {
@@ -659,10 +675,10 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
                                       blk->g_pad, feat + c, ld_feat, f16 + c, ld16, n16,
                                       blk->act, blk->slope, ws, ws_floats)
                : (dx3 && i < n_dx3)
-                   ? idf_conv3x3_dx3(stream, B, H, W, c, xs, nslab_xs, blk->dx3_w[i],
-                                     (blk->g_pad + 15) / 16, blk->dx3_yscale[i], blk->b3[i],
-                                     blk->vtap[i], blk->ldv, blk->bfull[i], blk->g_pad, feat + c,
-                                     ld_feat, blk->act, blk->slope, blk->range_flag)
+                   ? idf_conv3x3_dx3(stream, B, H, W, c, xs, nslab_xs, blk->dx3_w[i], dx3_nft,
+                                     blk->dx3_yscale[i], blk->b3[i], blk->vtap[i], blk->ldv,
+                                     blk->bfull[i], blk->g_pad, feat + c, ld_feat, blk->act,
+                                     blk->slope, blk->range_flag, dws, dws_bytes)
                : (wino && blk->wx3 && blk->wx3_u[i])
                    ? idf_conv3x3_wx3(stream, B, H, W, c, feat, ld_feat, blk->wx3_u[i],
                                      blk->wino_nft, blk->wx3_yscale[i], blk->b3[i], blk->vtap[i],

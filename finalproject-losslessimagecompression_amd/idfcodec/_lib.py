@@ -113,9 +113,11 @@ SIGNATURES = {
                                            i64, P, i64, i32, f32, P, i32, P, i64]),
     "idf_conv3x3_dx3_supported": (ctypes.c_int, [i32, i32, i32]),
     "idf_conv3x3_dx3": (ctypes.c_int, [P, i32, i32, i32, i32, P, i32, P, i32, f32, P, P, i32, P,
-                                       i32, P, i64, i32, f32, P]),
+                                       i32, P, i64, i32, f32, P, P, i64]),
+    "idf_conv3x3_dx3_counter_bytes": (i64, [i32, i32, i32, i32]),
+    "idf_conv3x3_dx3_workspace": (i64, [i32, i32, i32, i32, i32]),
     "idf_dx3_split_bytes": (i64, [i64, i32]),
-    "idf_dx3_split_cols": (ctypes.c_int, [P, i64, i32, i32, P, i64, P, i32, P]),
+    "idf_dx3_split_cols": (ctypes.c_int, [P, i64, i32, i32, P, i64, P, i32, P, P, i32]),
     "idf_conv3x3_bf16_workspace": (i64, [i32, i32, i32, i32, i32]),
     "idf_conv3x3_bf16": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, P, P, i32, P, i32,
                                         P, i64, P, i64, i32, i32, f32, P, i64]),

@@ -31,9 +31,13 @@ FLAG_CONV_X3 = 1
 # must run the same one.  Version 1 wrote 0 both for exact-f32 Winograd and for every engine
 # that predates the field (halo / gemm / unfold / bf16): a version-1 file with flags 0 reads as
 # conv "unrecorded", which any engine but a split-f16 one may decode (the pre-field behaviour).
-CONV_CODES = {"f32": 0, "x3": 1, "halo": 2, "gemm": 3, "unfold": 4, "bf16": 5, "dx3": 6}
+# 6: round 4's dx3 (direct split-f16 only at widths a multiple of 16: engine mode 'dx3w16');
+# 7: dx3 on every geometry conv3_dx3.hip packs (imagenet64's 8x8 level too)
+CONV_CODES = {"f32": 0, "x3": 1, "halo": 2, "gemm": 3, "unfold": 4, "bf16": 5, "dx3w16": 6,
+              "dx3": 7}
 # the split-f16 / exact-f32 modes one engine switches between per bitstream (engine.CONV_MODES)
-SWITCHABLE = ("dx3", "x3", "f32")
+SWITCHABLE = ("dx3", "dx3w16", "x3", "f32")
+SPLIT_F16 = ("dx3", "dx3w16", "x3")
 CONV_NAMES = {v: k for k, v in CONV_CODES.items()}
 
 
@@ -469,7 +473,7 @@ class ImageCodec:
         produced the streams is recorded in the bitstream (meta['conv'], container flag)."""
         eng = self.engine
         mode = eng.conv_family
-        if mode in ("x3", "dx3"):
+        if mode in SPLIT_F16:
             eng.clear_range_flag()
         nl = 1
         if lanes_img is not None and cond is None and not eng.conditional:
@@ -502,7 +506,7 @@ class ImageCodec:
             ws = load()
             eng.forward_pm(B, cond=cond, slot=slot)
             bs = self.coder.encode(ws, B, compact=compact)
-        if mode in ("x3", "dx3") and eng.range_flag_tripped():
+        if mode in SPLIT_F16 and eng.range_flag_tripped():
             eng.set_conv_mode("f32")
             try:
                 ws = load()
@@ -580,7 +584,7 @@ class ImageCodec:
                                  f"{bs.words.numel()} present")
         conv, have = bs.meta.get("conv", "f32"), eng.conv_family
         if conv == "unrecorded":  # version-1 file, flags 0: any engine but split-f16
-            if have in ("x3", "dx3"):
+            if have in SPLIT_F16:
                 raise ValueError("bitstream predates the conv field (version 1, flags 0) and "
                                  "was not coded with split-f16 convs; decode it with "
                                  "engine.set_conv_mode('f32') or the engine that wrote it")
@@ -588,7 +592,7 @@ class ImageCodec:
         if conv not in CONV_CODES:
             raise ValueError(f"unknown conv mode {conv!r}")
         switchable = conv in SWITCHABLE and have in SWITCHABLE and (
-            conv == "f32" or (conv == "x3" and eng.wx3) or (conv == "dx3" and eng.dx3))
+            conv == "f32" or (conv == "x3" and eng.wx3) or (conv in ("dx3", "dx3w16") and eng.dx3))
         if conv != have and not switchable:
             raise ValueError(f"bitstream was coded with {conv!r} convs; this engine runs "
                              f"{have!r} (IDF_FOLD / IDF_WINO / IDF_HALO / precision differ): "

@@ -29,7 +29,9 @@ from ._lib import IdfDenseBlock, IdfHeadOut, check, lib, ptr
 from .packing import PackedBlock, pack_dense_block, round_up
 
 FLOAT = 4
-CONV_MODES = ("dx3", "x3", "f32")
+CONV_MODES = ("dx3", "dx3w16", "x3", "f32")
+# the split-f16 modes (the range guard applies; fallback: exact-f32 "f32")
+SPLIT_F16 = ("dx3", "dx3w16", "x3")
 # Fold each DenseLayer's 1x1 conv into its 3x3 conv (packing.fold_layer): -46% of the
 # flow FLOPs at imagenet64; IDF_FOLD=0 runs the reference's two convolutions instead.
 FOLD = os.environ.get("IDF_FOLD", "1") != "0"
@@ -43,10 +45,12 @@ WINO = os.environ.get("IDF_WINO", "1") != "0"
 # hi/lo pair, three f16 MFMAs, f32 accumulation -- fp32-class error) with a
 # range guard that falls back to the exact-f32 kernel; IDF_WX3=0 always uses the latter.
 WX3 = os.environ.get("IDF_WX3", "1") != "0"
-# ... and, where the geometry allows (images a multiple of 16 wide: conv3_dx3.hip), as the direct
-# conv on the same split-f16 products with no transform ("dx3", the default mode: bench +1.4%
-# same-box, encode -0.8 ms); IDF_DX3=0 keeps every layer on wx3.  Conv modes: 'dx3' (dx3 where
-# supported, wx3 elsewhere), 'x3', 'f32'; the mode is recorded in the bitstream.
+# ... and, where the geometry allows (conv3_dx3.hip dx3_plan: widths a multiple of 16, packed
+# 8- and 4-wide images, bands of wider ones), as the direct conv on the same split-f16 products
+# with no transform ("dx3", the default mode); IDF_DX3=0 keeps every layer on wx3.  Conv modes:
+# 'dx3' (dx3 where supported, wx3 elsewhere), 'dx3w16' (round 4's dx3: only widths a multiple of
+# 16 on dx3 -- decodes version-2 files with conv code 6), 'x3', 'f32'; the mode is recorded in
+# the bitstream.
 DX3 = os.environ.get("IDF_DX3", "1") != "0"
 
 
@@ -290,9 +294,14 @@ class FlowEngine:
         ahead from ~188 channels."""
         return None
 
+    def _dx3_level_in(self, l: int, mode: str) -> bool:
+        """Level l's DenseLayers run on dx3 under conv mode `mode`."""
+        return mode in ("dx3", "dx3w16") and self._dx3_level(l) and (
+            mode == "dx3" or self.levels[l].w % 16 == 0)
+
     def dx3_layers(self, l: int, geom) -> int:
         """Leading layers of a level-l block with geometry `geom` that run on dx3."""
-        if not (self.conv_mode == "dx3" and self._dx3_level(l)):
+        if not self._dx3_level_in(l, self.conv_mode):
             return 0
         cm = self._dx3_cmax(l)
         return sum(1 for i in range(geom.depth) if cm is None or geom.k_in[i] <= cm)
@@ -306,18 +315,20 @@ class FlowEngine:
             raise ValueError(f"conv mode must be one of {CONV_MODES}, not {mode!r}")
         if mode == "x3" and not self.wx3:
             raise ValueError("this engine has no split-f16 (wx3) weights")
-        if mode == "dx3" and not self.dx3:
+        if mode in ("dx3", "dx3w16") and not self.dx3:
             raise ValueError("this engine has no split-f16 direct-conv (dx3) weights")
-        on = 1 if mode in ("x3", "dx3") else 0
-        for b in self._blocks:
-            b.desc.wx3 = on if b.wx3_u else 0
-            b.desc.dx3 = 1 if (mode == "dx3" and b.dx3_w and b.desc.wx3) else 0
+        on = 1 if mode in SPLIT_F16 else 0
+        for l in range(self.nsplit):
+            dl = self._dx3_level_in(l, mode)
+            for b in self.couple[l] + [self.prior[l]]:
+                b.desc.wx3 = on if b.wx3_u else 0
+                b.desc.dx3 = 1 if (dl and b.dx3_w and b.desc.wx3) else 0
         self.conv_mode = mode  # each mode's top prior is cached separately (_top_prior)
 
     @property
     def conv_family(self) -> str:
         """Which conv arithmetic produces the couplings -- the decoder must run the same one
-        (Bitstream.meta['conv']): 'dx3' / 'x3' / 'f32' (split-f16 direct + Winograd / split-f16
+        (Bitstream.meta['conv']): 'dx3' / 'dx3w16' / 'x3' / 'f32' (split-f16 direct + Winograd / split-f16
         Winograd / exact-f32 Winograd, switchable per bitstream), 'bf16', 'halo' (direct
         LDS-halo kernel), 'gemm' (folded implicit GEMM) or 'unfold' (the reference's 1x1 +
         3x3, IDF_FOLD=0)."""
@@ -371,7 +382,7 @@ class FlowEngine:
             "img": f(B * self.H * self.W * 4),
             "x": [[f(B * L.h * L.w * L.ldx), f(B * L.h * L.w * L.ldx)] for L in self.levels],
             "feat": f(Pmax * self.ld_feat),
-            "tmp": f(Pmax * self.ld_tmp),
+            "tmp": f(self._tmp_floats(B)),
             "lat": f(B * self.n_sym_img),
             "mean": f(B * self.n_sym_img),
             "logscale": f(B * self.n_sym_img),
@@ -387,6 +398,28 @@ class FlowEngine:
             self._ws.pop(next(iter(self._ws)))
         self._ws[(B, slot)] = ws
         return ws
+
+    def _tmp_floats(self, B: int) -> int:
+        """Floats of a workspace's tmp: P * ld_tmp at the widest level, and at every level room
+        for the dx3 layers' split copy (<= P * ld_tmp) plus their split-K workspace
+        (idf_conv3x3_dx3_workspace: the 8 x 8 level's partial sums)."""
+        n = 0
+        for l, Lv in enumerate(self.levels):
+            P = B * Lv.h * Lv.w
+            extra = 0
+            for b in self.couple[l] + [self.prior[l]]:
+                nd = len(b.dx3_w)
+                if nd:
+                    w = lib().idf_conv3x3_dx3_workspace(B, Lv.h, Lv.w, b.geom.k_in[nd - 1],
+                                                        b.geom.g_pad)
+                    extra = max(extra, int(w))
+            n = max(n, P * self.ld_tmp + ((extra + 256) // 4 + 16 * P if extra > 0 else 0))
+        return n
+
+    def tmp_pitch(self, ws, P: int) -> int:
+        """ld_tmp for a dense block of P pixels in ws['tmp']: the whole buffer as P rows (a
+        multiple of 16 floats), so the block sees every byte of it."""
+        return max(self.ld_tmp, (ws["tmp"].numel() // max(P, 1)) // 16 * 16)
 
     # ------------------------------------------------------------ pieces
     def _x(self, ws, l, which=0):
@@ -438,7 +471,7 @@ class FlowEngine:
             check(L.idf_copy_cols(s, P, 0, a_pad, None, 0, ptr(feat), ld), "zero cols")
         else:
             check(L.idf_copy_cols(s, P, nx, a_pad, x_src, ld_src, ptr(feat), ld), "copy cols")
-        blk.run(s, B, Lv.h, Lv.w, ptr(feat), ld, ptr(ws["tmp"]), self.ld_tmp,
+        blk.run(s, B, Lv.h, Lv.w, ptr(feat), ld, ptr(ws["tmp"]), self.tmp_pitch(ws, P),
                 head_prior(Lv.z, mean, logscale, scale))
 
     def ensure_top_prior(self, ws, s):
@@ -507,8 +540,8 @@ class FlowEngine:
                                               self.ld_feat), "permute")
                 self._swap(ws, l)
                 xo = ptr(x2) + Lv.a * FLOAT
-                blk.run(s, B, Lv.h, Lv.w, ptr(ws["feat"]), self.ld_feat, ptr(ws["tmp"]), self.ld_tmp,
-                        head_couple(_lib.EPI_COUPLE_ADD, xo, Lv.ldx))
+                blk.run(s, B, Lv.h, Lv.w, ptr(ws["feat"]), self.ld_feat, ptr(ws["tmp"]),
+                        self.tmp_pitch(ws, P), head_couple(_lib.EPI_COUPLE_ADD, xo, Lv.ldx))
                 yield l
             x, x2 = self._x(ws, l), self._x(ws, l, 1)
             check(L.idf_permute_couple_in(s, P, Lv.C, ptr(self.ids[l][self.nflows]), ptr(x), Lv.ldx,
@@ -598,8 +631,8 @@ class FlowEngine:
                 check(L.idf_copy_cols(s, P, Lv.a, blk.geom.a_pad, ptr(x), Lv.ldx, ptr(ws["feat"]),
                                       self.ld_feat), "copy cols")
                 xo = ptr(x) + Lv.a * FLOAT
-                blk.run(s, B, Lv.h, Lv.w, ptr(ws["feat"]), self.ld_feat, ptr(ws["tmp"]), self.ld_tmp,
-                        head_couple(_lib.EPI_COUPLE_SUB, xo, Lv.ldx))
+                blk.run(s, B, Lv.h, Lv.w, ptr(ws["feat"]), self.ld_feat, ptr(ws["tmp"]),
+                        self.tmp_pitch(ws, P), head_couple(_lib.EPI_COUPLE_SUB, xo, Lv.ldx))
                 check(L.idf_permute_couple_in(s, P, Lv.C, ptr(self.inv_ids[l][k]), ptr(x), Lv.ldx,
                                               ptr(x2), Lv.ldx, 0, 0, None, 0), "permute")
                 self._swap(ws, l)

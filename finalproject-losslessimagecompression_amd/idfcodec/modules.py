@@ -62,6 +62,20 @@ def _feat_from_nchw(x, db: DeviceBlock, extra_cols=0):
     return feat, ld, s
 
 
+def dense_tmp(db: DeviceBlock, B: int, H: int, W: int, ld_tmp: int, device):
+    """(tmp, its pitch) for one dense block run: P x ld_tmp floats, plus the dx3 layers'
+    split-K workspace where the geometry splits (idf_conv3x3_dx3_workspace)."""
+    P = B * H * W
+    n = P * ld_tmp
+    nd = len(db.dx3_w)
+    if nd and db.desc.dx3:
+        w = int(lib().idf_conv3x3_dx3_workspace(B, H, W, db.geom.k_in[nd - 1], db.geom.g_pad))
+        if w > 0:
+            n += (w + 256) // 4 + 16 * P
+    tmp = torch.empty(n, dtype=torch.float32, device=device)
+    return tmp, max(ld_tmp, (n // P) // 16 * 16)
+
+
 @torch.no_grad()
 def run_dense_block(block, x: torch.Tensor, fold=None) -> torch.Tensor:
     """DenseBlock.forward (nnblock.py:53-56) -> NCHW [B, o_channel, H, W]."""
@@ -82,7 +96,7 @@ def run_device_block(db: DeviceBlock, x: torch.Tensor, return_feat: bool = False
     ld_tmp = ld
     if db.desc.bf16:  # bf16 shadow of the features ahead of the split-K partials
         ld_tmp = max(ld, round_up(ld, 64) // 2 + 2 * 48 + 8)
-    tmp = torch.empty(P * ld_tmp, dtype=torch.float32, device=x.device)
+    tmp, ld_tmp = dense_tmp(db, B, H, W, ld_tmp, x.device)
     n = db.geom.n_head
     ldo = round_up(n, 4)
     out_pm = torch.empty(B * H * W * ldo, dtype=torch.float32, device=x.device)
@@ -131,10 +145,11 @@ def run_couple(couple, x: torch.Tensor, sign: int) -> torch.Tensor:
     check(lib().idf_nchw_to_pm(s, B, C, H, W, ptr(x.contiguous().float()), ptr(xpm), ldx), "nchw_to_pm")
     ld = db.geom.ld_feat
     feat = torch.empty(P * ld, dtype=torch.float32, device=x.device)
-    tmp = torch.empty_like(feat)
+    tmp, ld_tmp = dense_tmp(db, B, H, W, ld, x.device)
     check(lib().idf_copy_cols(s, P, couple.a_ch, db.geom.a_pad, ptr(xpm), ldx, ptr(feat), ld), "copy")
     mode = _lib.EPI_COUPLE_ADD if sign > 0 else _lib.EPI_COUPLE_SUB
-    db.run(s, B, H, W, ptr(feat), ld, ptr(tmp), ld, head_couple(mode, ptr(xpm) + couple.a_ch * FLOAT, ldx))
+    db.run(s, B, H, W, ptr(feat), ld, ptr(tmp), ld_tmp,
+           head_couple(mode, ptr(xpm) + couple.a_ch * FLOAT, ldx))
     out = torch.empty((B, C, H, W), dtype=torch.float32, device=x.device)
     check(lib().idf_pm_to_nchw(s, B, C, H, W, ptr(xpm), ldx, ptr(out)), "pm_to_nchw")
     return out
@@ -148,10 +163,11 @@ def run_prior(prior, inp: torch.Tensor):
     x = inp if prior.cond_channel > 0 else torch.zeros_like(inp)
     B, C, H, W = x.shape
     feat, ld, s = _feat_from_nchw(x, db)
-    tmp = torch.empty_like(feat)
+    tmp, ld_tmp = dense_tmp(db, B, H, W, ld, x.device)
     n = prior.out_channel
     mean = torch.empty((B, n, H, W), dtype=torch.float32, device=x.device)
     logs = torch.empty_like(mean)
     scale = torch.empty_like(mean)
-    db.run(s, B, H, W, ptr(feat), ld, ptr(tmp), ld, head_prior(n, ptr(mean), ptr(logs), ptr(scale)))
+    db.run(s, B, H, W, ptr(feat), ld, ptr(tmp), ld_tmp,
+           head_prior(n, ptr(mean), ptr(logs), ptr(scale)))
     return mean, logs

@@ -198,35 +198,45 @@ def x3_scale(U: np.ndarray) -> int:
     return max(-14, min(k, 60))
 
 
+def dx3_groups(n_alloc: int):
+    """(fragments per group, groups) of a dx3 layer with n_alloc (a multiple of 16) outputs:
+    one kernel block computes up to 4 fragments of 16 outputs (conv3_dx3.hip dx3_plan)."""
+    nft = max(1, n_alloc // 16)
+    nf = min(nft, 4)
+    return nf, (nft + nf - 1) // nf
+
+
 def dx3_weights(w: np.ndarray, C: int):
     """Split-f16 direct-conv weights for idf_conv3x3_dx3 (conv3_dx3.hip).
 
     w: [n_alloc, 9, ldw] folded 3x3 weights (float64 preferred) in the padded channel
     coordinates, C = the layer's padded input channels.  Scaled by 2^k (x3_scale: max |w| 2^k
     in [2^14, 2^15)) and split wh = f16(w'), wl = f16(w' - wh), both round-to-nearest-even.
-    Returns (uint16 [nslab][2: hi, lo][9 taps][nft][16 out][16 ch], yscale = 2^-k): per slab
-    the A-operand (output-row) fragments the kernel stages into LDS verbatim; channels at or
-    past C are zero."""
+    Returns (uint16 [nslab][ngroup][2: hi, lo][9 taps][nf][16 out][16 ch], yscale = 2^-k): per
+    slab and output group the A-operand (output-row) fragments one kernel block stages into LDS
+    verbatim; channels at or past C are zero.  nf = min(n_alloc / 16, 4) fragments per group,
+    ngroup = ceil(n_alloc / 16 / nf) groups (dx3_groups; outputs past n_alloc are zero)."""
     n_alloc = w.shape[0]
     assert n_alloc % 16 == 0
-    nft = n_alloc // 16
+    nf, ngroup = dx3_groups(n_alloc)
+    nft = nf * ngroup
     nslab = (C + 15) // 16
-    wp = np.zeros((n_alloc, 9, nslab * 16), np.float64)
+    wp = np.zeros((nft * 16, 9, nslab * 16), np.float64)
     cw = min(C, w.shape[2])
-    wp[:, :, :cw] = w[:, :, :cw]
+    wp[:n_alloc, :, :cw] = w[:, :, :cw]
     k = x3_scale(wp)
     ws = wp * (2.0 ** k)
     hi = ws.astype(np.float16)
     lo = (ws - hi.astype(np.float64)).astype(np.float16)
-    out = np.empty((nslab, 2, 9, nft, 16, 16), np.uint16)
+    out = np.empty((nslab, ngroup, 2, 9, nf, 16, 16), np.uint16)
     for t, part in enumerate((hi, lo)):
-        p = part.view(np.uint16).reshape(nft, 16, 9, nslab, 16)  # f, r, tap, slab, c
-        out[:, t] = p.transpose(3, 2, 0, 1, 4)
+        p = part.view(np.uint16).reshape(ngroup, nf, 16, 9, nslab, 16)  # g, f, r, tap, slab, c
+        out[:, :, t] = p.transpose(4, 0, 3, 1, 2, 5)
     # The kernel's invariant (conv3_dx3.hip, "split copy"): a layer reads its input's last slab
     # up to the next multiple of 16 channels, i.e. also channels [C, 16 nslab) that other
     # blocks of the same launch are writing (its own outputs).  Those channels must meet
     # exactly +0 weights (hi and lo), so any finite value there adds exactly +-0.
-    assert C % 16 == 0 or not out[-1, :, :, :, :, C % 16:].any(), "dx3 weights past C not zero"
+    assert C % 16 == 0 or not out[-1, ..., C % 16:].any(), "dx3 weights past C not zero"
     return np.ascontiguousarray(out), float(2.0 ** -k)
 
 

@@ -334,28 +334,41 @@ int idf_conv3x3_wx3_res(void *stream, int32_t B, int32_t H, int32_t W, int32_t C
  * no VALU in the k-loop (conv3_dx3.hip).  The input is the block's SPLIT feature copy
  * d_xs [nslab_xs][2: hi, lo][P = B*H*W][16] f16 (idf_dx3_split_bytes bytes for 16*nslab_xs
  * channels), staged by LDS-DMA; channels [0, C) are read.  d_w: uint16
- * [ceil(C/16) slabs][2: hi, lo][9 taps][nft][16 outputs][16 channels] (idfcodec/packing.py
- * dx3_weights), nft = ceil(N/16) <= 3.  Writes the N outputs as fp32 to d_out (16-B aligned,
- * ld_out a multiple of 4) AND as split pairs to d_xs channels [C, C + N), with zeros on to the
- * next multiple of 16 past C + N (so the next layer's last slab holds finite values).
- * Geometry: W a multiple of 16 (idf_conv3x3_dx3_supported; 16x16 output tiles, any H).  Range
+ * [ceil(C/16) slabs][ngroup][2: hi, lo][9 taps][nf][16 outputs][16 channels]
+ * (idfcodec/packing.py dx3_weights): nft = ngroup * nf fragments of 16 outputs, nf =
+ * min(ceil(N/16), 4), ngroup = ceil(ceil(N/16) / nf) (one block per group).  Writes the N
+ * outputs as fp32 to d_out (16-B aligned, ld_out a multiple of 4) AND as split pairs to d_xs
+ * channels [C, C + N), with zeros on to the next multiple of 16 past C + N (so the next layer's
+ * last slab holds finite values).  Geometry (idf_conv3x3_dx3_supported): 16 x 16 output tiles
+ * of W a multiple of 16 (any H); of 2 x 2 / 4 x 4 packed images W = 8 / 4 (H 4 or 8 packed
+ * down the tile too, other H in 16-row tiles); of bands of images W > 16 side by side (any H).
+ * Where the tiles are few for any batch (H * W <= 64 with <= 4 images a tile: imagenet64's
+ * 8 x 8 level) the slabs split into up to 4 fixed chunks whose partial sums the last block of
+ * a tile adds in chunk order: then d_workspace (256-B aligned, idf_conv3x3_dx3_workspace bytes)
+ * holds the per-tile counters in its first idf_conv3x3_dx3_counter_bytes bytes -- zero at the
+ * call, left zero by it (idf_dx3_split_cols clears them) -- and the partial sums after them.
+ * The tiling, chunks and summation order depend on (H, W, C, N) only, never on B.  Range
  * guard: bit 0 of *d_flag when a stored output is NaN or |y| >= 8192.  The outputs differ from
  * wx3's in the last bits (another fixed summation order), so an encoder and its decoder run the
  * same one (Bitstream conv code 'dx3').  Replaces the reference's DenseLayer conv
  * (nnlayer.py:48-51, 1x1 folded in, nnblock.py:53-56). */
 int idf_conv3x3_dx3_supported(int32_t H, int32_t W, int32_t N);
 int64_t idf_dx3_split_bytes(int64_t P, int32_t channels);
+int64_t idf_conv3x3_dx3_counter_bytes(int32_t B, int32_t H, int32_t W, int32_t N);
+int64_t idf_conv3x3_dx3_workspace(int32_t B, int32_t H, int32_t W, int32_t C, int32_t N);
 /* The block input's split copy: d_xs channels [c0, c1) (c0 a multiple of 16, c1 of 4) of the P
  * fp32 rows d_x (ld_x floats), zeros for [c1, round16(c1)); bit 0 of *d_flag when an input is
- * NaN or |x| >= 32768 (the f16 pairs' range).  Replaces nothing in the reference: the split
- * form of the DenseBlock input (nnblock.py:53-56) the dx3 layers read. */
+ * NaN or |x| >= 32768 (the f16 pairs' range); also clears d_zero[0, nzero) (the dx3 layers'
+ * split-K counters; NULL / 0: none).  Replaces nothing in the reference: the split form of the
+ * DenseBlock input (nnblock.py:53-56) the dx3 layers read. */
 int idf_dx3_split_cols(void *stream, int64_t P, int32_t c0, int32_t c1, const float *d_x,
-                       int64_t ld_x, uint16_t *d_xs, int32_t nslab_xs, uint32_t *d_flag);
+                       int64_t ld_x, uint16_t *d_xs, int32_t nslab_xs, uint32_t *d_flag,
+                       uint32_t *d_zero, int32_t nzero);
 int idf_conv3x3_dx3(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, uint16_t *d_xs,
                     int32_t nslab_xs, const uint16_t *d_w, int32_t nft, float yscale,
                     const float *d_b3, const float *d_vtap, int32_t ldv, const float *d_bfull,
                     int32_t N, float *d_out, int64_t ld_out, int32_t act, float slope,
-                    uint32_t *d_flag);
+                    uint32_t *d_flag, void *d_workspace, int64_t workspace_bytes);
 
 /* The same folded 3x3 conv on bf16 MFMA (v_mfma_f32_16x16x32_bf16, fp32 accumulation).
  * The input is the bf16 shadow d_x16 of the fp32 feature columns (ld_x16 a multiple of 8,

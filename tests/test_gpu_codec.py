@@ -110,10 +110,10 @@ def test_coder_api_chained_round_trip(golden):
 
 
 def test_conv_modes_and_range_guard_fallback(monkeypatch):
-    """imagenet64 runs the split-f16 direct convs where the geometry allows (conv 'dx3': the
-    32x32 and 16x16 levels; the 8x8 level keeps split-f16 Winograd); a bitstream records the
-    conv mode, the decoder follows it whatever mode the engine is in (dx3 / x3 / f32), and a
-    tripped range guard re-encodes the batch with the exact-f32 convs."""
+    """imagenet64 runs the split-f16 direct convs at every level (conv 'dx3'; 'dx3w16' is
+    round 4's: direct at 32x32 / 16x16, Winograd at 8x8, container code 6); a bitstream records
+    the conv mode, the decoder follows it whatever mode the engine is in (dx3 / dx3w16 / x3 /
+    f32), and a tripped range guard re-encodes the batch with the exact-f32 convs."""
     from idfcodec import synthetic
     from idfcodec.codec import Bitstream
     model = _imagenet64()
@@ -129,13 +129,18 @@ def test_conv_modes_and_range_guard_fallback(monkeypatch):
     eng.set_conv_mode("f32")
     bs_f32 = codec.encode(img)
     assert bs_f32.meta["conv"] == "f32"
+    eng.set_conv_mode("dx3w16")
+    bs_w16 = codec.encode(img)
+    assert bs_w16.meta["conv"] == "dx3w16"
+    assert Bitstream.from_bytes(bs_w16.to_bytes()).meta["conv"] == "dx3w16"
     eng.set_conv_mode("dx3")
     # the modes give (slightly) different couplings, so different streams, all lossless
-    for a_, b_ in ((bs_dx3, bs_x3), (bs_x3, bs_f32), (bs_dx3, bs_f32)):
+    for a_, b_ in ((bs_dx3, bs_x3), (bs_x3, bs_f32), (bs_dx3, bs_f32), (bs_dx3, bs_w16)):
         assert not (torch.equal(a_.states, b_.states) and torch.equal(a_.words, b_.words))
-    for bs in (bs_dx3, bs_x3, bs_f32, Bitstream.from_bytes(bs_f32.to_bytes(), "cuda"),
+    for bs in (bs_dx3, bs_x3, bs_f32, bs_w16, Bitstream.from_bytes(bs_f32.to_bytes(), "cuda"),
                Bitstream.from_bytes(bs_x3.to_bytes(), "cuda"),
-               Bitstream.from_bytes(bs_dx3.to_bytes(), "cuda")):
+               Bitstream.from_bytes(bs_dx3.to_bytes(), "cuda"),
+               Bitstream.from_bytes(bs_w16.to_bytes(), "cuda")):
         out, info = codec.decode(bs)
         assert info["ok"] and torch.equal(out.cpu(), img.cpu()), bs.meta
         assert eng.conv_mode == "dx3"

@@ -60,17 +60,33 @@ def xs_channels(xs, P, nslab, c0, c1):
     return a[..., 0], a[..., 1]
 
 
+def dx3_workspace(B, H, W, C, N, dev):
+    """(zeroed workspace, bytes, counter bytes) for idf_conv3x3_dx3 (None, 0, 0 when the
+    geometry does not split K)."""
+    from idfcodec._lib import lib
+    n = int(lib().idf_conv3x3_dx3_workspace(B, H, W, C, N))
+    assert n >= 0
+    if n == 0:
+        return None, 0, 0
+    ctr = int(lib().idf_conv3x3_dx3_counter_bytes(B, H, W, N))
+    assert 0 < ctr < n and ctr % 256 == 0
+    return torch.zeros(n // 4, dtype=torch.int32, device=dev), n, ctr
+
+
 def run_dx3(cs, act, X=None, B=None, layer2=False):
     """split_cols of the input, then one dx3 layer (or two: the second reads the first's split
     outputs).  Returns (out, flag, xs, P, nslab_xs[, X after layer 1])."""
     from idfcodec import _lib
     from idfcodec._lib import check, lib, ptr
-    from idfcodec.packing import dx3_weights
+    from idfcodec.packing import dx3_groups, dx3_weights
     B = cs["B"] if B is None else B
     X = (cs["X"] if X is None else X).clone()
     H, W, C, N, ld, n_alloc = cs["H"], cs["W"], cs["C"], cs["N"], cs["ld"], cs["n_alloc"]
+    assert lib().idf_conv3x3_dx3_supported(H, W, N) == 1
     P = B * H * W
     dev = torch.device("cuda")
+    nf, ngroup = dx3_groups(n_alloc)
+    nft = nf * ngroup
     Wd, ysc = dx3_weights(cs["Wt"].numpy(), C)
     Wdd = torch.from_numpy(Wd.view(np.int16)).to(dev)
     Xd, b3d = X.to(dev), cs["b3"].to(dev)
@@ -82,27 +98,38 @@ def run_dx3(cs, act, X=None, B=None, layer2=False):
     nslab = (c_top + 15) // 16
     xs = torch.full((nslab * 2 * P * 16,), F16_NAN, dtype=torch.int16, device=dev)
     assert lib().idf_dx3_split_bytes(P, nslab * 16) == xs.numel() * 2
+    ws, wsb, ctr = dx3_workspace(B, H, W, C + (N if layer2 else 0), N, dev)
     s = _lib.stream_ptr()
-    check(lib().idf_dx3_split_cols(s, P, 0, C, ptr(Xd), ld, ptr(xs), nslab, ptr(flag)), "split")
+    check(lib().idf_dx3_split_cols(s, P, 0, C, ptr(Xd), ld, ptr(xs), nslab, ptr(flag), None, 0),
+          "split")
+
+    def counters_zero():  # every launch leaves the split-K tile counters zero
+        if ws is not None:
+            torch.cuda.synchronize()
+            assert not ws[:ctr // 4].any(), "dx3 left a split-K counter non-zero"
+
     if not layer2:
-        check(lib().idf_conv3x3_dx3(s, B, H, W, C, ptr(xs), nslab, ptr(Wdd), n_alloc // 16, ysc,
+        check(lib().idf_conv3x3_dx3(s, B, H, W, C, ptr(xs), nslab, ptr(Wdd), nft, ysc,
                                     ptr(b3d), ptr(vtd), n_alloc, ptr(bfd), N, ptr(out), ld,
-                                    _lib.ACT[act], 0.01, ptr(flag)), "dx3")
+                                    _lib.ACT[act], 0.01, ptr(flag), ptr(ws), wsb), "dx3")
         torch.cuda.synchronize()
+        counters_zero()
         return out.cpu(), int(flag.item()), xs.cpu(), P, nslab
     # layer 1 writes its fp32 outputs into X[:, C:C+N] and the split ones into xs
-    check(lib().idf_conv3x3_dx3(s, B, H, W, C, ptr(xs), nslab, ptr(Wdd), n_alloc // 16, ysc,
+    check(lib().idf_conv3x3_dx3(s, B, H, W, C, ptr(xs), nslab, ptr(Wdd), nft, ysc,
                                 ptr(b3d), ptr(vtd), n_alloc, ptr(bfd), N, ptr(Xd) + 4 * C, ld,
-                                _lib.ACT[act], 0.01, ptr(flag)), "dx3 layer 1")
+                                _lib.ACT[act], 0.01, ptr(flag), ptr(ws), wsb), "dx3 layer 1")
+    counters_zero()
     C2 = C + N
     W2 = torch.from_numpy(np.random.default_rng(C2).normal(0, 1 / np.sqrt(9 * C2), (n_alloc, 9, C2)))
     W2[N:] = 0.0
     Wd2, ysc2 = dx3_weights(W2.numpy(), C2)
     Wdd2 = torch.from_numpy(Wd2.view(np.int16)).to(dev)
-    check(lib().idf_conv3x3_dx3(s, B, H, W, C2, ptr(xs), nslab, ptr(Wdd2), n_alloc // 16, ysc2,
+    check(lib().idf_conv3x3_dx3(s, B, H, W, C2, ptr(xs), nslab, ptr(Wdd2), nft, ysc2,
                                 ptr(b3d), ptr(vtd), n_alloc, ptr(bfd), N, ptr(out), ld,
-                                _lib.ACT[act], 0.01, ptr(flag)), "dx3 layer 2")
+                                _lib.ACT[act], 0.01, ptr(flag), ptr(ws), wsb), "dx3 layer 2")
     torch.cuda.synchronize()
+    counters_zero()
     return out.cpu(), int(flag.item()), xs.cpu(), P, nslab, Xd.cpu(), W2
 
 
@@ -152,7 +179,20 @@ def got_nchw(out, cs):
     (2, 64, 64, 8, 16, "LeakyReLU", True), (2, 20, 32, 24, 32, "ReLU", True),
     (2, 16, 48, 12, 43, "LeakyReLU", True), (1, 5, 16, 40, 44, "ReLU", True),
     (4, 16, 16, 36, 12, "ReLU", False), (2, 32, 32, 100, 48, "LeakyReLU", True),
-    (3, 17, 16, 20, 44, "None", True)])
+    (3, 17, 16, 20, 44, "None", True),
+    # packed tiles: 8x8 images 2x2 to a tile with K split in 4 chunks (imagenet64's 8x8
+    # level: a partial last band, 1 slab a chunk, 9 slabs a chunk), one group of 1 fragment
+    (5, 8, 8, 36, 44, "ReLU", True), (6, 8, 8, 520, 44, "ReLU", True),
+    (4, 8, 8, 52, 44, "ReLU", True), (2, 8, 8, 12, 16, "LeakyReLU", True),
+    # 4x4 images 4x4 to a tile (config 4's first level): 64 outputs (4 fragments), 128 (two
+    # groups of 4), a partial band
+    (3, 4, 4, 100, 64, "ReLU", True), (2, 4, 4, 36, 128, "ReLU", True),
+    (17, 4, 4, 20, 64, "ReLU", True),
+    # bands of images with one edge inside a tile: 23-wide (config 5's patches, 27 rows: two
+    # 16-row tiles), 24- and 40-wide (8-wide offsets), 8-wide with rows that do not pack
+    (3, 27, 23, 40, 32, "LeakyReLU", True), (2, 8, 24, 20, 44, "ReLU", True),
+    (1, 8, 40, 20, 44, "ReLU", True), (2, 5, 8, 24, 44, "ReLU", True),
+    (2, 16, 8, 24, 44, "ReLU", True)])
 def test_dx3_vs_fp64(B, H, W, C, N, act, fold):
     cs = make_case(B, H, W, C, N, fold)
     out, flag, xs, P, nslab = run_dx3(cs, act)
@@ -181,7 +221,9 @@ def test_dx3_vs_fp64(B, H, W, C, N, act, fold):
 
 
 @pytest.mark.parametrize("B,H,W,C,act", [(2, 32, 32, 52, "ReLU"), (3, 16, 16, 100, "LeakyReLU"),
-                                         (1, 16, 32, 496, "ReLU"), (2, 9, 16, 8, "ReLU")])
+                                         (1, 16, 32, 496, "ReLU"), (2, 9, 16, 8, "ReLU"),
+                                         (6, 8, 8, 100, "ReLU"), (5, 4, 4, 36, "ReLU"),
+                                         (3, 27, 23, 24, "LeakyReLU")])
 def test_dx3_two_layers_through_the_split_copy(B, H, W, C, act):
     """Layer 2 reads layer 1's split outputs (the producer side of the split copy): equal, within
     the 1e-5 contract, to an fp64 conv of layer 1's fp32 outputs."""
@@ -240,9 +282,51 @@ def test_dx3_output_guard_sets_flag():
     assert run_dx3(cs, "None")[1] == 0
 
 
-def test_dx3_unsupported_geometry():
+def test_dx3_supported_geometry():
+    """The packed tilings cover imagenet64's three levels and configs 4/5's first levels;
+    2-wide images (config 4's 2x2 level: a 32 x 32-slot canvas), widths below 16 that do not
+    divide it and 4-row 8-wide images (a 15 KiB plane) stay on wx3."""
     from idfcodec._lib import lib
-    assert lib().idf_conv3x3_dx3_supported(32, 32, 44) == 1
-    assert lib().idf_conv3x3_dx3_supported(8, 8, 44) == 0
-    assert lib().idf_conv3x3_dx3_supported(27, 23, 32) == 0
-    assert lib().idf_conv3x3_dx3_supported(16, 16, 64) == 0
+    L = lib()
+    for H, W, N in ((32, 32, 44), (16, 16, 44), (8, 8, 44), (27, 23, 32), (16, 16, 64),
+                    (4, 4, 64), (4, 4, 128), (8, 40, 44), (5, 8, 44)):
+        assert L.idf_conv3x3_dx3_supported(H, W, N) == 1, (H, W, N)
+    for H, W, N in ((2, 2, 64), (2, 2, 128), (8, 12, 44), (4, 8, 44), (7, 7, 44), (2, 4, 64)):
+        assert L.idf_conv3x3_dx3_supported(H, W, N) == 0, (H, W, N)
+    # split K only where the tiles are few for any batch: the 8x8 level
+    assert L.idf_conv3x3_dx3_workspace(256, 8, 8, 520, 44) > 0
+    assert L.idf_conv3x3_dx3_workspace(256, 8, 8, 12, 44) == 0  # one slab: nothing to split
+    assert L.idf_conv3x3_dx3_workspace(256, 16, 16, 520, 44) == 0
+    assert L.idf_conv3x3_dx3_workspace(256, 4, 4, 520, 64) == 0
+
+
+def test_dx3_split_k_batch_invariant():
+    """8x8 images (split K, 2x2 images a tile): an image's outputs are the same bits alone, in
+    another tile position and inside a batch -- the chunks are summed in chunk order whichever
+    block finishes last."""
+    cs = make_case(9, 8, 8, 300, 44, True, seed=5)
+    full = run_dx3(cs, "ReLU")[0]
+    again = run_dx3(cs, "ReLU")[0]
+    assert torch.equal(full, again)
+    P = 64
+    for i in (0, 3, 8):
+        one = cs["X"][i * P: (i + 1) * P].clone()
+        alone = run_dx3(cs, "ReLU", X=one, B=1)[0]
+        assert torch.equal(full[i * P: (i + 1) * P], alone), i
+    # two images: the second at tile position 1 (top right) instead of i % 4
+    two = cs["X"][7 * P: 9 * P].clone()
+    pair = run_dx3(cs, "ReLU", X=two, B=2)[0]
+    assert torch.equal(full[7 * P: 9 * P], pair)
+
+
+def test_dx3_packed_batch_invariant():
+    """4x4 images (16 a tile) and 27x23 images (bands of 16, one edge inside a tile): outputs
+    are the same bits at any position in any batch."""
+    for B, H, W, C, N in ((21, 4, 4, 60, 64), (19, 27, 23, 40, 32)):
+        cs = make_case(B, H, W, C, N, True, seed=B)
+        full = run_dx3(cs, "LeakyReLU")[0]
+        P = H * W
+        for i in (0, 5, B - 1):
+            one = cs["X"][i * P: (i + 1) * P].clone()
+            alone = run_dx3(cs, "LeakyReLU", X=one, B=1)[0]
+            assert torch.equal(full[i * P: (i + 1) * P], alone), (H, W, i)

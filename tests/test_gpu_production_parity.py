@@ -50,7 +50,7 @@ def in64():
     model = synthetic.build_model(configs.get("imagenet64")).cuda()
     eng = model.engine()
     assert eng.conv_mode == "dx3" and eng.wx3 and eng.dx3, \
-        "imagenet64 must run the split-f16 convs (direct at 32x32 / 16x16, Winograd at 8x8)"
+        "imagenet64 must run the split-f16 direct convs (32x32 / 16x16 tiles; 8x8 packed 2x2)"
     return model, eng
 
 
@@ -87,8 +87,8 @@ def _layer_out(feat, geom, i):
 @pytest.mark.parametrize("lvl", [0, 1, 2])
 def test_imagenet64_x3_blocks_teacher_forced(in64, lvl, mode):
     """Every DenseBlock of level `lvl` as the engine packed it, in both split-f16 modes: 'dx3'
-    (the default: the direct conv at the 32x32 and 16x16 levels, Winograd at 8x8) and 'x3'
-    (Winograd everywhere)."""
+    (the default: the direct conv at every level -- 16x16 tiles at 32x32 and 16x16, 2x2 packed
+    8x8 images with K split in 4 chunks at 8x8) and 'x3' (Winograd everywhere)."""
     import flow_oracle as FO
     from idfcodec.modules import run_device_block
     model, eng = in64
@@ -106,7 +106,8 @@ def _x3_blocks_teacher_forced(model, eng, lvl, mode, FO, run_device_block):
     worst_block = worst_layer = 0.0
     for name, mod, db in _blocks(model, eng, lvl):
         assert db.desc.wino and db.desc.wx3, (name, "not on the split-f16 path")
-        assert db.desc.dx3 == (1 if mode == "dx3" and Lv.w % 16 == 0 else 0), (name, mode)
+        assert db.desc.dx3 == (1 if eng._dx3_level_in(lvl, mode) else 0), (name, mode)
+        assert db.desc.dx3 == (1 if mode == "dx3" else 0), (name, mode)  # every level, round 5
         c_in = mod.i_channel
         x = _grid((2, c_in, hw, hw), g)
         sd = {k: v.detach().cpu() for k, v in mod.state_dict().items()}

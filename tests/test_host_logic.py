@@ -316,22 +316,27 @@ def test_bf16_weight_packing_layout():
 
 
 def test_dx3_weight_packing_layout_and_prefix(golden):
-    """dx3_weights: [slab][hi, lo][tap][nft][out][ch] f16 pairs with (hi + lo) 2^-k equal to
-    the float64 weight within f16-pair precision, zeros past C; pack_dense_block(dx3_cmax)
-    packs them for the leading layers whose input is at most dx3_cmax wide, nothing after."""
+    """dx3_weights: [slab][group][hi, lo][tap][nf][out][ch] f16 pairs with (hi + lo) 2^-k equal
+    to the float64 weight within f16-pair precision, zeros past C (and past n_alloc in the last
+    group); groups of up to 4 fragments (dx3_groups); pack_dense_block(dx3_cmax) packs them for
+    the leading layers whose input is at most dx3_cmax wide, nothing after."""
     import numpy as np
-    from idfcodec.packing import dx3_weights, pack_dense_block
+    from idfcodec.packing import dx3_groups, dx3_weights, pack_dense_block
+    assert [dx3_groups(n) for n in (16, 48, 64, 80, 128, 192)] == \
+        [(1, 1), (3, 1), (4, 1), (4, 2), (4, 2), (4, 3)]
     rng = np.random.default_rng(6)
-    n_alloc, C, ldw = 48, 40, 48
-    w = rng.normal(0, 0.05, (n_alloc, 9, ldw))
-    w[:, :, C:] = 0
-    d, ysc = dx3_weights(w, C)
-    assert d.shape == (3, 2, 9, 3, 16, 16) and d.dtype == np.uint16
-    f = d.view(np.float16).astype(np.float64)
-    back = (f[:, 0] + f[:, 1]) * ysc                       # slab, tap, nft, out, ch
-    back = back.transpose(2, 3, 1, 0, 4).reshape(n_alloc, 9, 48)
-    assert np.abs(back[:, :, :C] - w[:, :, :C]).max() <= 2.0 ** -20 * np.abs(w).max()
-    assert not back[:, :, C:].any()
+    for n_alloc, C, ldw, shape in ((48, 40, 48, (3, 1, 2, 9, 3, 16, 16)),
+                                   (80, 36, 48, (3, 2, 2, 9, 4, 16, 16))):
+        w = rng.normal(0, 0.05, (n_alloc, 9, ldw))
+        w[:, :, C:] = 0
+        d, ysc = dx3_weights(w, C)
+        assert d.shape == shape and d.dtype == np.uint16
+        f = d.view(np.float16).astype(np.float64)
+        back = (f[:, :, 0] + f[:, :, 1]) * ysc               # slab, group, tap, nf, out, ch
+        nft = shape[1] * shape[4]
+        back = back.transpose(1, 3, 4, 2, 0, 5).reshape(nft * 16, 9, shape[0] * 16)
+        assert np.abs(back[:n_alloc, :, :C] - w[:, :, :C]).max() <= 2.0 ** -20 * np.abs(w).max()
+        assert not back[:, :, C:].any() and not back[n_alloc:].any()
     g = golden("flow_t1_idflows_2lvl.npz")
     cfg = yaml.safe_load(bytes(g["cfg_yaml"]).decode())
     sd = {k[3:]: torch.from_numpy(g[k]) for k in g.files if k.startswith("sd/")}
