@@ -57,6 +57,7 @@ namespace idf {
 typedef float d4 __attribute__((ext_vector_type(4)));
 typedef _Float16 e4 __attribute__((ext_vector_type(4)));
 typedef _Float16 e8 __attribute__((ext_vector_type(8)));
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
 struct Dx3Args {
   const uint16_t* xs;  // split features [nslab_xs][2: hi, lo][P][16] f16 bits
@@ -141,12 +142,30 @@ __device__ unsigned long long g_dx3_phase[8][6];
 #define DX3_STAMP(slab, j) do { } while (0)
 #define DX3_PHASE(j, v) do { } while (0)
 #endif
+// timing-only block timeline (IDF_DX3_TL=1 builds): per block, wave 0 lane 0 -- s_memrealtime
+// (100 MHz, chip-wide) at entry, after the bias table, after slab 0's barrier, at the loop's end,
+// after the split-K hand-off (last block only) and at the end; read back with idf_dx3_timeline
+#ifndef IDF_DX3_TL
+#define IDF_DX3_TL 0
+#endif
+#if IDF_DX3_TL
+__device__ unsigned long long g_dx3_tl[4096][8];
+#define DX3_TL(j)                                                                          \
+  do {                                                                                    \
+    if (tid == 0 && blockIdx.x < 4096) g_dx3_tl[blockIdx.x][(j)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define DX3_TL(j) do { } while (0)
+#endif
 // the waves that issue the DMA pieces: IDF_DX3_DMAW of them from wave IDF_DX3_DMAW0
 #ifndef IDF_DX3_DMAW
 #define IDF_DX3_DMAW IDF_DX3_WAVES
 #endif
 #ifndef IDF_DX3_DMAW0
 #define IDF_DX3_DMAW0 0
+#endif
+#ifndef IDF_DX3_KSPLIT
+#define IDF_DX3_KSPLIT 4  // chunks of the split-K levels (timing A/B builds only: changes bits)
 #endif
 // 1: one tile per block at every geometry (timing A/B of the two block shapes)
 #ifndef IDF_DX3_FORCE1
@@ -338,12 +357,14 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
 #pragma unroll
     for (int i = 0; i < L::PPW; ++i) dma(s0, 0, i);
   }
+  DX3_TL(0);
   for (int e = tid; e < NF * 512 / 16; e += kDxThreads) *(d4*)(lds + L::ZOFF + 16 * e) = d4{0.f, 0.f, 0.f, 0.f};
   DX3_PHASE(0, __builtin_amdgcn_s_memtime());
   DX3_PHASE(4, __builtin_amdgcn_s_memrealtime());
   stage_bias((float*)(lds + L::BOFF), NF * 16, grp * NF * 16, g.N, g.b3, g.vtap, g.bfull, g.ldv,
              tid, kDxThreads);
   DX3_PHASE(1, __builtin_amdgcn_s_memtime());
+  DX3_TL(1);
 
   // ---- the wave's canvas position: lane j's column base (its segment's base + its offset in
   // the segment; = j mod 8) and the wave's first canvas row (its rows lie in one image)
@@ -444,6 +465,7 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!(IDF_DX3_ABLATE & 8)) __builtin_amdgcn_s_barrier();
     DX3_STAMP(s - s0, 1);
+    if (s == s0) DX3_TL(2);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy) read_A(cur, 0, dy, AS[0][dy]);
@@ -505,42 +527,70 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
     DX3_STAMP(s - s0, 3);
   }
   DX3_PHASE(2, __builtin_amdgcn_s_memtime());
+  DX3_TL(3);
 
   // ---- split K: every chunk's block stores its raw sums; the tile's last block to finish
-  // adds them in chunk order (its own from registers -- the same bits) and runs the epilogue
-  if (g.nchunk > 1) {
+  // adds them in chunk order (its own from registers -- the same bits) and runs the epilogue.
+  // The hand-off within the launch (MI355X_MICROARCH.md "Valid forms", table row 1): payload
+  // stored write-through (sc1, 16 B a lane), every storing wave drained (vmcnt 0), a workgroup
+  // barrier, ONE lane's agent-scope atomic add on the tile's counter; the block whose add
+  // returns nchunk - 1 is last, resets the counter and reads every chunk with sc1 loads (which
+  // bypass this CU's L1) -- no release / acquire fences, whose L2 write-back costs microseconds
+  // per block.
+  // (compiled only into the one-tile blocks: the host splits K only with T = 1)
+  if constexpr (T == 1) if (g.nchunk > 1) {
     constexpr int FR = kDxWaves * WR * NF;  // fragments per block
-    const int64_t pb = ((int64_t)(tb * g.ngroup + grp) * g.nchunk) * FR * 64;  // d4 index of chunk 0
-    d4* part = (d4*)g.part;
+    const uint32_t pb = (uint32_t)((tb * g.ngroup + grp) * g.nchunk) * (FR * 1024u);  // bytes
+    const int64_t pbytes = (int64_t)g.nblk_tiles * g.ngroup * g.nchunk * FR * 1024;
+    const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)g.part, 0, (int)(pbytes < (int64_t)kDxInvalid ? pbytes : (int64_t)kDxInvalid), 0x00020000);
+    auto poff = [&](int c, int m, int n) -> uint32_t {
+      return pb + (uint32_t)((c * FR + (wave * WR + m) * NF + n) * 1024 + lane * 16);
+    };
 #pragma unroll
     for (int m = 0; m < WR; ++m)
 #pragma unroll
       for (int n = 0; n < NF; ++n)
-        part[pb + ((int64_t)chunk * FR + (wave * WR + m) * NF + n) * 64 + lane] = acc[m][n];
-    __threadfence();  // release: this wave's partials visible at agent scope
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[m][n]), pr, poff(chunk, m, n),
+                                               0, 16 /* sc1 */);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
     __syncthreads();
     if (tid == 0) {
-      // wraps to 0 at the last arrival: the counter is zero again for the next launch
-      const uint32_t old = __builtin_amdgcn_atomic_inc32(g.ctr + tb * g.ngroup + grp,
-                                                         (uint32_t)(g.nchunk - 1), __ATOMIC_ACQ_REL,
-                                                         "agent");
-      *last_flag = old == (uint32_t)(g.nchunk - 1);
+      const uint32_t old = __hip_atomic_fetch_add(g.ctr + tb * g.ngroup + grp, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+      const bool last = old == (uint32_t)(g.nchunk - 1);
+      if (last)  // no other block touches it again in this launch: zero for the next one
+        __hip_atomic_store(g.ctr + tb * g.ngroup + grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *last_flag = last;
     }
     __syncthreads();
+    DX3_TL(6);
     if (!*last_flag) return;
-    __threadfence();  // acquire: the other chunks' partials
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below
+    // every other chunk's fragments in flight at once (one memory round trip, not nchunk), then
+    // the sums in chunk order; chunk slots past nchunk and the block's own read nothing
+    static_assert(IDF_DX3_KSPLIT <= 4, "the reduction holds up to 4 chunks");
+    d4 pv[4][WR][NF];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int m = 0; m < WR; ++m)
+#pragma unroll
+        for (int n = 0; n < NF; ++n)
+          pv[c][m][n] = (c < g.nchunk && c != chunk)
+                            ? __builtin_bit_cast(d4, __builtin_amdgcn_raw_buffer_load_b128(pr, poff(c, m, n), 0, 16))
+                            : acc[m][n];
 #pragma unroll
     for (int m = 0; m < WR; ++m)
 #pragma unroll
       for (int n = 0; n < NF; ++n) {
-        d4 sum = chunk == 0 ? acc[m][n] : part[pb + ((int64_t)(wave * WR + m) * NF + n) * 64 + lane];
-        for (int c = 1; c < g.nchunk; ++c) {
-          const d4 v = c == chunk ? acc[m][n]
-                                  : part[pb + ((int64_t)c * FR + (wave * WR + m) * NF + n) * 64 + lane];
-          sum = sum + v;
-        }
+        d4 sum = pv[0][m][n];
+#pragma unroll
+        for (int c = 1; c < 4; ++c)
+          if (c < g.nchunk) sum = sum + pv[c][m][n];
         acc[m][n] = sum;
       }
+    DX3_TL(4);
   }
 
   // ---- epilogue: lane holds outputs 16 (grp NF + n) + 4q .. +3 of packed pixel (row r0 + m,
@@ -598,6 +648,7 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
     }
   }
   if (!out_ok && g.flag) atomicOr(g.flag, 1u);
+  DX3_TL(5);
   DX3_PHASE(3, __builtin_amdgcn_s_memtime());
   DX3_PHASE(5, __builtin_amdgcn_s_memrealtime());
 }
@@ -640,9 +691,6 @@ __global__ void __launch_bounds__(256) dx3_split_cols_kernel(int64_t P, int32_t 
 // ---- geometry plan (host): how a (H, W, N) layer tiles, packs and splits.  A function of the
 // image geometry, the output count and C only -- never of the batch -- so an encoder and its
 // decoder run every layer with the same tiles, chunks and summation order.
-#ifndef IDF_DX3_KSPLIT
-#define IDF_DX3_KSPLIT 4  // chunks of the split-K levels (timing A/B builds only: changes bits)
-#endif
 struct Dx3Plan {
   int ok, pitch, plane_kib, nbx, nby, ch, seg, segw, nseg, modeb, nf, ngroup, split;
 };
@@ -692,6 +740,12 @@ static Dx3Plan dx3_plan(int H, int W, int N) {
 }  // namespace idf
 
 using namespace idf;
+
+#if IDF_DX3_TL
+extern "C" int idf_dx3_timeline(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dx3_tl), sizeof(g_dx3_tl)) == hipSuccess ? 0 : 2;
+}
+#endif
 
 #if IDF_DX3_STAMPS
 extern "C" int idf_dx3_stamps(unsigned long long* host) {

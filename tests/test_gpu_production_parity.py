@@ -294,8 +294,14 @@ def test_config45_x3_blocks_teacher_forced(cfg45, name, lvl):
     B = 37 if H * W <= 16 else 3  # a ragged count of packed small patches
     g = torch.Generator().manual_seed(300 + lvl + 17 * len(name))
     worst = 0.0
+    # round 5: dx3 (packed tiles) wherever conv3_dx3.hip tiles the level -- config 4's 4x4 level
+    # (16 patches a tile, 64 / 128 outputs in groups of 4 fragments) and config 5's 27x23 level
+    # (bands of 16 patches); config 4's 2x2 level stays on wx3
+    want_dx3 = {("resflows_smallpatch_split", 0): 1, ("resflows_smallpatch_split", 1): 0,
+                ("resflow-patches-vqvae", 0): 1}[(name, lvl)]
     for bname, mod, db in _blocks(fl, eng, lvl):
         assert db.desc.wino and db.desc.wx3, (name, bname, "not on the split-f16 Winograd path")
+        assert db.desc.dx3 == want_dx3, (name, lvl, bname, db.desc.dx3)
         x = _grid((B, mod.i_channel, H, W), g)
         sd = {k: v.detach().cpu() for k, v in mod.state_dict().items()}
         eng.clear_range_flag()
@@ -314,7 +320,7 @@ def test_config45_x3_blocks_teacher_forced(cfg45, name, lvl):
         assert torch.equal(again, out), (bname, "re-run differs")
         part, _ = run_device_block(db, x[1:3].contiguous().cuda())
         assert torch.equal(part, out[1:3]), (bname, "images 1-2 alone differ from the batch")
-    print(f"{name} level {lvl} ({H}x{W}): worst whole-block {worst:.2e}")
+    print(f"{name} level {lvl} ({H}x{W}, dx3={want_dx3}): worst whole-block {worst:.2e}")
 
 
 def _sampled_streams_vs_oracle(oracle, fl, rbs, seed, n_pick=24):
@@ -352,7 +358,7 @@ def test_config45_full_size_streams_vs_oracle(oracle, name, src, B):
     codec, fl, vq, size = synthetic.build_residual(name)
     x = synthetic.images(B, H=src[0], W=src[1], seed=23).cuda()
     rbs = codec.encode(x)
-    assert rbs.vq_conv == "x3" and rbs.flow.meta.get("conv") == "x3"
+    assert rbs.vq_conv == "x3" and rbs.flow.meta.get("conv") == "dx3"
     n = _sampled_streams_vs_oracle(oracle, fl, rbs, seed=len(name))
     assert n >= 10
     out, info = codec.decode(rbs)

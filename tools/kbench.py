@@ -88,16 +88,41 @@ def main():
             WD, dsc = dx3_weights(np.random.default_rng(0).normal(0, 0.01, (g_alloc, 9, ldw)), c_pad)
             WD = torch.from_numpy(WD.view(np.int16)).to(dev)
             xs = None
+            dws, dwn = None, 0
             if "dx3" in only:
                 nsx = (c_pad + g_pad + 15) // 16
                 xs = torch.empty(nsx * 2 * P * 16, dtype=torch.int16, device=dev)
-                check(lib().idf_dx3_split_cols(s, P, 0, c_pad, ptr(feat), ld, ptr(xs), nsx, ptr(flag)),
-                      "split")
+                check(lib().idf_dx3_split_cols(s, P, 0, c_pad, ptr(feat), ld, ptr(xs), nsx, ptr(flag),
+                                               None, 0), "split")
+                dwn = int(lib().idf_conv3x3_dx3_workspace(B, hw, hw, c_pad, g_pad))
+                if dwn > 0:  # split K: zeroed counters (each launch leaves them zero)
+                    dws = torch.zeros(dwn // 4, dtype=torch.int32, device=dev)
 
             def dx3():
                 check(lib().idf_conv3x3_dx3(s, B, hw, hw, c_pad, ptr(xs), nsx, ptr(WD), g_alloc // 16,
                                             dsc, ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
-                                            ptr(feat) + c_pad * 4, ld, 0, 0.0, ptr(flag)), "dx3")
+                                            ptr(feat) + c_pad * 4, ld, 0, 0.0, ptr(flag), ptr(dws),
+                                            dwn), "dx3")
+
+            # KB_ONLY=dx3r4: round 4's dx3 kernel (tools/ab_lib/dx3_r4/libdx3old.so, built from
+            # that commit's conv3_dx3.hip) on the same box, same data -- its old ABI
+            old = None
+            if "dx3r4" in only:
+                import ctypes
+                old = ctypes.CDLL(os.path.join(REPO, "tools", "ab_lib", "dx3_r4", "libdx3old.so"))
+                P_, i32_, i64_, f32_ = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float
+                old.idf_conv3x3_dx3.argtypes = [P_, i32_, i32_, i32_, i32_, P_, i32_, P_, i32_, f32_,
+                                                P_, P_, i32_, P_, i32_, P_, i64_, i32_, f32_, P_]
+                if xs is None:
+                    nsx = (c_pad + g_pad + 15) // 16
+                    xs = torch.empty(nsx * 2 * P * 16, dtype=torch.int16, device=dev)
+                    check(lib().idf_dx3_split_cols(s, P, 0, c_pad, ptr(feat), ld, ptr(xs), nsx,
+                                                   ptr(flag), None, 0), "split")
+
+            def dx3r4():
+                check(old.idf_conv3x3_dx3(s, B, hw, hw, c_pad, ptr(xs), nsx, ptr(WD), g_alloc // 16,
+                                          dsc, ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
+                                          ptr(feat) + c_pad * 4, ld, 0, 0.0, ptr(flag)), "dx3r4")
 
             from idfcodec.packing import bf16_weights
             WB = torch.from_numpy(bf16_weights(np.random.default_rng(1).normal(
@@ -120,8 +145,8 @@ def main():
                                                  g_alloc, ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
                                                  ptr(feat) + c_pad * 4, ld, 0, 0.0), "gemm")
             line = f"L{lvl} hw={hw:2d} c={c_pad:4d} P={P:7d}"
-            for name, fn in (("wino", wino), ("wx3", wx3), ("dx3", dx3), ("halo", halo), ("gemm", gemm),
-                             ("bf16", bf16)):
+            for name, fn in (("wino", wino), ("wx3", wx3), ("dx3", dx3), ("dx3r4", dx3r4),
+                             ("halo", halo), ("gemm", gemm), ("bf16", bf16)):
                 if name not in only:
                     continue
                 ms = time_it(fn, reps)
