@@ -73,7 +73,8 @@ struct Dx3Args {
   int32_t tiles_x, tiles_y, ntiles, nblk_tiles;
   int32_t ch;           // canvas rows
   int32_t seg, segw, nseg;  // segment stride and width (slots), segments per canvas
-  int32_t modeb;        // 1: at most two segments side by side in a row (runtime split)
+  int32_t gut, wp, hp;  // 1: gutter packing -- images at pitch wp = W + 1 across, hp = H + 1
+                        // down, the zero row / column between two images shared by both
   // split K
   int32_t nchunk, chunk_slabs;
   float* part;          // [nblk_tiles][ngroup][nchunk][waves][WR][NF][64 lanes] d4
@@ -218,11 +219,11 @@ __device__ __forceinline__ void dx_unroll(F&& f, std::integer_sequence<int, T...
 }
 
 // A tile's place in the packed layout: band (nbx x nby images), first packed column u0 and row
-// u0y, the image column ix0 / row iy0 they fall in, the first column's image x (xf0), the first
-// lane of the next image column (jc; >= 16: none), the canvas row 0's vertical coordinate vy0
-// (canvas row cr holds packed vertical coordinate vy0 + cr, image row vy / (H + 2)).
+// u0y; with segments, the image column ix0 / row iy0 they fall in, the first column's image x
+// (xf0) and the canvas row 0's vertical coordinate vy0 (canvas row cr holds packed vertical
+// coordinate vy0 + cr, image row vy / (H + 2)).
 struct DxTile {
-  int band, u0, ix0, xf0, jc, u0y, iy0, vy0;
+  int band, u0, ix0, xf0, u0y, iy0, vy0;
 };
 
 __device__ __forceinline__ DxTile dx_tile(const Dx3Args& g, int tile) {
@@ -235,7 +236,6 @@ __device__ __forceinline__ DxTile dx_tile(const Dx3Args& g, int tile) {
   t.u0 = 16 * tx;
   t.ix0 = udiv_s(t.u0, g.Wd);
   t.xf0 = t.u0 - t.ix0 * g.Wd;
-  t.jc = (t.ix0 + 1) * g.Wd - t.u0;
   t.u0y = 16 * ty;
   t.iy0 = udiv_s(t.u0y, g.H);
   if (t.iy0 > g.nby - 1) t.iy0 = g.nby - 1;
@@ -293,30 +293,28 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
       const int tt = tb * T + t;
       if (tt < g.ntiles) {
         const DxTile dt = dx_tile(g, tt);
-        // canvas slot -> (segment, canvas row, segment column)
-        int sk, cr, cc;
+        // canvas slot -> image (ix, iy) of the band and pixel (x, y)
+        int ix, x, iy, y;
         bool ok;
-        if (g.modeb) {
-          cr = slot / PITCH;
-          const int col = slot - cr * PITCH;
-          const int b1 = dt.jc + 8;  // segment 1's first slot in a row
-          sk = (dt.jc < 16 && col >= b1) ? 1 : 0;
-          cc = col - (sk ? b1 : 0);
-          const int width = sk ? 16 - dt.jc + 2 : (dt.jc < 16 ? dt.jc : 16) + 2;
-          ok = cc < width;
-        } else {
-          sk = g.seg ? udiv_s(slot, g.seg) : 0;
+        if (g.gut) {  // one 18 x 18 canvas of packed pixels; gutters and edges read zero
+          const int cr = slot / PITCH, cc = slot - cr * PITCH;
+          const int u = dt.u0 - 1 + cc, uy = dt.u0y - 1 + cr;
+          ix = u >= 0 ? udiv_s(u, g.wp) : 0;
+          x = u >= 0 ? u - ix * g.wp : -1;
+          iy = uy >= 0 ? udiv_s(uy, g.hp) : 0;
+          y = uy >= 0 ? uy - iy * g.hp : -1;
+          ok = cr < g.ch && cc < g.segw;
+        } else {  // canvas slot -> (segment, canvas row, segment column)
+          const int sk = g.seg ? udiv_s(slot, g.seg) : 0;
           const int rr = slot - sk * g.seg;
-          cr = rr / PITCH;
-          cc = rr - cr * PITCH;
-          ok = sk < g.nseg && cc < g.segw;
+          const int cr = rr / PITCH, cc = rr - cr * PITCH;
+          ok = sk < g.nseg && cc < g.segw && cr < g.ch;
+          ix = dt.ix0 + sk;
+          x = (sk ? 0 : dt.xf0) - 1 + cc;
+          const int vy = dt.vy0 + cr;
+          iy = udiv_s(vy, g.H + 2);
+          y = vy - iy * (g.H + 2) - 1;
         }
-        ok = ok && cr < g.ch;
-        const int ix = dt.ix0 + sk;
-        const int x = (sk ? 0 : dt.xf0) - 1 + cc;
-        const int vy = dt.vy0 + cr;
-        const int iy = udiv_s(vy, g.H + 2);
-        const int y = vy - iy * (g.H + 2) - 1;
         const int b = (dt.band * g.nby + iy) * g.nbx + ix;
         ok = ok && x >= 0 && x < g.Wd && ix < g.nbx && y >= 0 && y < g.H && iy < g.nby && b < g.B;
         if (ok)
@@ -366,20 +364,21 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   DX3_PHASE(1, __builtin_amdgcn_s_memtime());
   DX3_TL(1);
 
-  // ---- the wave's canvas position: lane j's column base (its segment's base + its offset in
-  // the segment; = j mod 8) and the wave's first canvas row (its rows lie in one image)
+  // ---- the wave's canvas position: lane j's column base (gutter packing: j; segments: its
+  // segment's base + its offset in the segment, = j mod 8) and the wave's first canvas row
+  // (segments: its rows lie in one image)
   const int j = lane & 15, q = lane >> 4;
   const DxTile dt = dx_tile(g, tile < g.ntiles ? tile : 0);
   const int uj = dt.u0 + j;
-  const int ixj = udiv_s(uj, g.Wd);           // lane j's image column in the band
-  const int xj = uj - ixj * g.Wd;             // and its x
+  const int pw = g.gut ? g.wp : g.Wd;
+  const int ixj = udiv_s(uj, pw);             // lane j's image column in the band
+  const int xj = uj - ixj * pw;               // and its x (gutter packing: W = the gutter)
   const int kj = ixj - dt.ix0;                // its segment
-  const int colb = g.modeb ? (kj ? dt.jc + 8 + (j - dt.jc) : j)
-                           : kj * g.seg + (kj ? j - (ixj * g.Wd - dt.u0) : j);
+  const int colb = g.gut ? j : kj * g.seg + (kj ? j - (ixj * g.Wd - dt.u0) : j);
   const int uyw = dt.u0y + r0;
   int iyw = udiv_s(uyw, g.H);
   if (iyw > g.nby - 1) iyw = g.nby - 1;
-  const int rowb = uyw + 2 * iyw - dt.vy0;    // canvas row of the wave's halo row 0
+  const int rowb = g.gut ? r0 : uyw + 2 * iyw - dt.vy0;  // canvas row of the wave's halo row 0
 
   // ---- fragment read offsets (bytes from a stage base).  B (pixels): lane (q = lane >> 4,
   // j = lane & 15) reads pixel j of a canvas row, 8 channels.  A (weights): output j, 8 channels.
@@ -599,8 +598,7 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   // 16-channel boundary past C + N, so the next layer's last slab reads finite values; never
   // past the split buffer).
   if (tile >= g.ntiles) return;
-  const int b_img = (dt.band * g.nby + iyw) * g.nbx + ixj;
-  if (b_img >= g.B) return;
+  if (xj >= g.Wd || ixj >= g.nbx) return;  // a gutter column or past the band (gutter packing)
   const WAct act(g.act, g.slope);
   const float* btab = (const float*)(lds + L::BOFF);
   bool out_ok = true;
@@ -609,8 +607,13 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   char* xsb = (char*)g.xs;
 #pragma unroll
   for (int m = 0; m < WR; ++m) {
-    const int y = uyw + m - iyw * g.H;
-    if (y >= g.H) continue;
+    int iy = iyw, y = uyw + m - iyw * g.H;
+    if (g.gut) {
+      iy = udiv_s(uyw + m, g.hp);
+      y = uyw + m - iy * g.hp;
+    }
+    const int b_img = (dt.band * g.nby + iy) * g.nbx + ixj;
+    if (y >= g.H || iy >= g.nby || b_img >= g.B) continue;
     const int cls = bias_class(y, xj, g.H, g.Wd);
     const int64_t pix = ((int64_t)b_img * g.H + y) * g.Wd + xj;
     float* dst = g.out + pix * g.ldo;
@@ -692,7 +695,7 @@ __global__ void __launch_bounds__(256) dx3_split_cols_kernel(int64_t P, int32_t 
 // image geometry, the output count and C only -- never of the batch -- so an encoder and its
 // decoder run every layer with the same tiles, chunks and summation order.
 struct Dx3Plan {
-  int ok, pitch, plane_kib, nbx, nby, ch, seg, segw, nseg, modeb, nf, ngroup, split;
+  int ok, pitch, plane_kib, nbx, nby, ch, seg, segw, nseg, gut, wp, hp, nf, ngroup, split;
 };
 
 static int dx3_gcd(int a, int b) { return b ? dx3_gcd(b, a % b) : a; }
@@ -703,37 +706,44 @@ static Dx3Plan dx3_plan(int H, int W, int N) {
   const int nft = (N + 15) / 16;
   p.nf = nft <= 4 ? nft : 4;
   p.ngroup = (nft + p.nf - 1) / p.nf;
-  if (W % 16 == 0) {  // 16-wide tiles of one image, any H
-    p.nbx = 1; p.pitch = 18; p.segw = 18; p.nseg = 1; p.plane_kib = 11;
-  } else if (W == 4 || W == 8) {  // 16 / W images across a tile, one segment each
+  if (W % 16 == 0) {  // 16-wide tiles of one image, any H (16-row tiles)
+    p.nbx = 1; p.nby = 1; p.pitch = 18; p.ch = 18; p.segw = 18; p.nseg = 1; p.plane_kib = 11;
+    p.ok = 1;
+  } else if (W == 4 || W == 8) {
+    // 16 / W images across a tile, one canvas segment each (every lane an output); H = 2, 4, 8
+    // stacked down the tile too, with gutter rows in the segment
     p.nbx = 16 / W; p.pitch = W + 2; p.segw = W + 2; p.nseg = p.nbx;
     p.plane_kib = W == 8 ? 13 : 19;
-  } else if (W > 16) {  // bands of nbx images (a multiple of 16 wide): <= one edge per tile
-    p.nbx = 16 / dx3_gcd(W, 16); p.pitch = 26; p.modeb = 1; p.nseg = 2; p.plane_kib = 17;
-  } else {
-    return p;
-  }
-  if (p.nbx > 1 && (H == 2 || H == 4 || H == 8)) {  // images stacked down a tile, gutter rows
-    p.nby = 16 / H;
-    p.ch = p.nby * (H + 2);
-  } else {
-    p.nby = 1;
-    p.ch = 18;
-  }
-  int slots = p.ch * p.pitch;
-  if (!p.modeb && p.nseg > 1) {
+    if (H == 2 || H == 4 || H == 8) {
+      p.nby = 16 / H;
+      p.ch = p.nby * (H + 2);
+    } else {
+      p.nby = 1;
+      p.ch = 18;
+    }
     // segment stride = W (mod 8) slots: lane j's column base is then j (mod 8) in every
     // segment, so the fragment reads stay bank-conflict-free
-    int s = p.ch * p.pitch;
-    while ((s - W) % 8) ++s;
-    p.seg = s;
-    slots = p.nseg * s;
+    int sg = p.ch * p.pitch;
+    while ((sg - W) % 8) ++sg;
+    p.seg = sg;
+    p.ok = (p.nseg * sg * 32 + 1023) / 1024 <= p.plane_kib;
   }
-  if ((slots * 32 + 1023) / 1024 > p.plane_kib) return p;
+  if (!p.ok) {
+    // gutter packing (any other geometry): images at pitch W + 1 across and H + 1 down in bands
+    // of nbx x nby whose packed extent is a whole number of 16-pixel tiles where that fits in
+    // 8 tiles; the one zero column / row between two images is both images' padding, so the
+    // canvas is the plain 18 x 18 one and a gutter lane's output is simply not stored
+    p.gut = 1; p.wp = W + 1; p.hp = H + 1;
+    p.nbx = 16 / dx3_gcd(p.wp, 16);
+    while (p.nbx > 1 && p.nbx * p.wp > 128) p.nbx /= 2;
+    p.nby = 16 / dx3_gcd(p.hp, 16);
+    while (p.nby > 1 && p.nby * p.hp > 128) p.nby /= 2;
+    p.pitch = 18; p.ch = 18; p.segw = 18; p.nseg = 1; p.seg = 0; p.plane_kib = 11;
+    p.ok = 1;
+  }
   // split K where a level's tiles are few for any batch the bench runs (imagenet64's 8 x 8:
   // 64 tiles per 256 images): by the geometry alone
   p.split = (H * W <= 64 && p.nbx * p.nby <= 4) ? IDF_DX3_KSPLIT : 1;
-  p.ok = 1;
   return p;
 }
 
@@ -756,6 +766,10 @@ extern "C" int idf_dx3_stamps(unsigned long long* host) {
 
 namespace {
 
+// tiles across / down one band of the plan's packing
+int dx3_tiles_x(const Dx3Plan& p, int W) { return (p.nbx * (p.gut ? p.wp : W) + 15) / 16; }
+int dx3_tiles_y(const Dx3Plan& p, int H) { return (p.nby * (p.gut ? p.hp : H) + 15) / 16; }
+
 struct Dx3Launch {
   Dx3Plan pl;
   int64_t ntiles;
@@ -770,7 +784,7 @@ Dx3Launch dx3_launch_shape(int B, int H, int W, int C, int N) {
   s.pl = dx3_plan(H, W, N);
   if (!s.pl.ok || B < 1) return s;
   const int64_t nbands = (B + s.pl.nbx * s.pl.nby - 1) / (s.pl.nbx * s.pl.nby);
-  const int tiles_x = s.pl.nbx * W / 16, tiles_y = (s.pl.nby * H + 15) / 16;
+  const int tiles_x = dx3_tiles_x(s.pl, W), tiles_y = dx3_tiles_y(s.pl, H);
   s.ntiles = nbands * tiles_x * tiles_y;
   s.nslab = (C + 15) / 16;
   s.chunk_slabs = s.nslab > 0 ? (s.nslab + s.pl.split - 1) / s.pl.split : 1;
@@ -865,11 +879,12 @@ extern "C" int idf_conv3x3_dx3(void* stream, int32_t B, int32_t H, int32_t W, in
   g.Wt = w; g.nslab = sh.nslab; g.ngroup = sh.pl.ngroup; g.N = N;
   g.B = B; g.H = H; g.Wd = W;
   g.nbx = sh.pl.nbx; g.nby = sh.pl.nby;
-  g.tiles_x = sh.pl.nbx * W / 16;
-  g.tiles_y = (sh.pl.nby * H + 15) / 16;
+  g.tiles_x = dx3_tiles_x(sh.pl, W);
+  g.tiles_y = dx3_tiles_y(sh.pl, H);
   g.ntiles = (int32_t)sh.ntiles;
   g.nblk_tiles = sh.nblk_tiles;
-  g.ch = sh.pl.ch; g.seg = sh.pl.seg; g.segw = sh.pl.segw; g.nseg = sh.pl.nseg; g.modeb = sh.pl.modeb;
+  g.ch = sh.pl.ch; g.seg = sh.pl.seg; g.segw = sh.pl.segw; g.nseg = sh.pl.nseg;
+  g.gut = sh.pl.gut; g.wp = sh.pl.wp; g.hp = sh.pl.hp;
   g.nchunk = sh.nchunk; g.chunk_slabs = sh.chunk_slabs;
   g.b3 = b3; g.vtap = vtap; g.bfull = bfull; g.ldv = ldv; g.act = act; g.slope = slope;
   g.out = out; g.ldo = ld_out; g.yscale = yscale; g.flag = d_flag;
@@ -895,10 +910,8 @@ extern "C" int idf_conv3x3_dx3(void* stream, int32_t B, int32_t H, int32_t W, in
     IDF_DX3_NF(W2, 18, 11)
   } else if (sh.pl.pitch == 10) {
     IDF_DX3_NF(W2, 10, 13)
-  } else if (sh.pl.pitch == 6) {
-    IDF_DX3_NF(W2, 6, 19)
   } else {
-    IDF_DX3_NF(W2, 26, 17)
+    IDF_DX3_NF(W2, 6, 19)
   }
 #undef IDF_DX3_NF
 #undef IDF_DX3_GO

@@ -339,9 +339,10 @@ int idf_conv3x3_wx3_res(void *stream, int32_t B, int32_t H, int32_t W, int32_t C
  * min(ceil(N/16), 4), ngroup = ceil(ceil(N/16) / nf) (one block per group).  Writes the N
  * outputs as fp32 to d_out (16-B aligned, ld_out a multiple of 4) AND as split pairs to d_xs
  * channels [C, C + N), with zeros on to the next multiple of 16 past C + N (so the next layer's
- * last slab holds finite values).  Geometry (idf_conv3x3_dx3_supported): 16 x 16 output tiles
- * of W a multiple of 16 (any H); of 2 x 2 / 4 x 4 packed images W = 8 / 4 (H 4 or 8 packed
- * down the tile too, other H in 16-row tiles); of bands of images W > 16 side by side (any H).
+ * last slab holds finite values).  Geometry (idf_conv3x3_dx3_supported: any H, W): 16 x 16
+ * output tiles of W a multiple of 16; of 16 / W images across (W = 8 or 4; H = 2, 4, 8 also
+ * stacked down) in canvas segments; of any other geometry "gutter-packed" -- images at pitch
+ * W + 1 across and H + 1 down, one zero column / row shared by neighbours.
  * Where the tiles are few for any batch (H * W <= 64 with <= 4 images a tile: imagenet64's
  * 8 x 8 level) the slabs split into up to 4 fixed chunks whose partial sums the last block of
  * a tile adds in chunk order: then d_workspace (256-B aligned, idf_conv3x3_dx3_workspace bytes)

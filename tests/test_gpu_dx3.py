@@ -188,10 +188,14 @@ def got_nchw(out, cs):
     # groups of 4), a partial band
     (3, 4, 4, 100, 64, "ReLU", True), (2, 4, 4, 36, 128, "ReLU", True),
     (17, 4, 4, 20, 64, "ReLU", True),
-    # bands of images with one edge inside a tile: 23-wide (config 5's patches, 27 rows: two
-    # 16-row tiles), 24- and 40-wide (8-wide offsets), 8-wide with rows that do not pack
+    # gutter packing (images at pitch W + 1 / H + 1, the zero column / row between two images
+    # shared): 27x23 (config 5's patches, 2 x 4 a band), 24- and 40-wide, 2x2 (config 4's
+    # second level: 16 x 16 a band, 128 outputs), 7x7, 12x12, 8-wide with 4 rows (its segment
+    # canvas would not fit); 8-wide segments with rows that do not pack
     (3, 27, 23, 40, 32, "LeakyReLU", True), (2, 8, 24, 20, 44, "ReLU", True),
-    (1, 8, 40, 20, 44, "ReLU", True), (2, 5, 8, 24, 44, "ReLU", True),
+    (1, 8, 40, 20, 44, "ReLU", True), (37, 2, 2, 24, 128, "ReLU", True),
+    (5, 7, 7, 20, 44, "ReLU", True), (3, 12, 12, 36, 44, "LeakyReLU", True),
+    (6, 4, 8, 40, 44, "ReLU", True), (2, 5, 8, 24, 44, "ReLU", True),
     (2, 16, 8, 24, 44, "ReLU", True)])
 def test_dx3_vs_fp64(B, H, W, C, N, act, fold):
     cs = make_case(B, H, W, C, N, fold)
@@ -223,7 +227,7 @@ def test_dx3_vs_fp64(B, H, W, C, N, act, fold):
 @pytest.mark.parametrize("B,H,W,C,act", [(2, 32, 32, 52, "ReLU"), (3, 16, 16, 100, "LeakyReLU"),
                                          (1, 16, 32, 496, "ReLU"), (2, 9, 16, 8, "ReLU"),
                                          (6, 8, 8, 100, "ReLU"), (5, 4, 4, 36, "ReLU"),
-                                         (3, 27, 23, 24, "LeakyReLU")])
+                                         (3, 27, 23, 24, "LeakyReLU"), (40, 2, 2, 20, "ReLU")])
 def test_dx3_two_layers_through_the_split_copy(B, H, W, C, act):
     """Layer 2 reads layer 1's split outputs (the producer side of the split copy): equal, within
     the 1e-5 contract, to an fp64 conv of layer 1's fp32 outputs."""
@@ -283,15 +287,15 @@ def test_dx3_output_guard_sets_flag():
 
 
 def test_dx3_supported_geometry():
-    """The packed tilings cover imagenet64's three levels and configs 4/5's first levels;
-    2-wide images (config 4's 2x2 level: a 32 x 32-slot canvas), widths below 16 that do not
-    divide it and 4-row 8-wide images (a 15 KiB plane) stay on wx3."""
+    """The tilings (16-wide tiles, packed segments, gutter packing) cover every image geometry:
+    imagenet64's three levels and configs 4/5's; only more than 1024 outputs are refused."""
     from idfcodec._lib import lib
     L = lib()
     for H, W, N in ((32, 32, 44), (16, 16, 44), (8, 8, 44), (27, 23, 32), (16, 16, 64),
-                    (4, 4, 64), (4, 4, 128), (8, 40, 44), (5, 8, 44)):
+                    (4, 4, 64), (4, 4, 128), (8, 40, 44), (5, 8, 44), (2, 2, 64), (2, 2, 128),
+                    (8, 12, 44), (4, 8, 44), (7, 7, 44), (2, 4, 64), (1, 1, 16), (64, 64, 1024)):
         assert L.idf_conv3x3_dx3_supported(H, W, N) == 1, (H, W, N)
-    for H, W, N in ((2, 2, 64), (2, 2, 128), (8, 12, 44), (4, 8, 44), (7, 7, 44), (2, 4, 64)):
+    for H, W, N in ((8, 8, 1025), (0, 8, 44), (8, 8, 0)):
         assert L.idf_conv3x3_dx3_supported(H, W, N) == 0, (H, W, N)
     # split K only where the tiles are few for any batch: the 8x8 level
     assert L.idf_conv3x3_dx3_workspace(256, 8, 8, 520, 44) > 0
@@ -320,9 +324,9 @@ def test_dx3_split_k_batch_invariant():
 
 
 def test_dx3_packed_batch_invariant():
-    """4x4 images (16 a tile) and 27x23 images (bands of 16, one edge inside a tile): outputs
-    are the same bits at any position in any batch."""
-    for B, H, W, C, N in ((21, 4, 4, 60, 64), (19, 27, 23, 40, 32)):
+    """4x4 images (16 a tile, segments), 27x23 and 2x2 images (gutter packing): outputs are the
+    same bits at any position in any batch."""
+    for B, H, W, C, N in ((21, 4, 4, 60, 64), (19, 27, 23, 40, 32), (300, 2, 2, 24, 128)):
         cs = make_case(B, H, W, C, N, True, seed=B)
         full = run_dx3(cs, "LeakyReLU")[0]
         P = H * W

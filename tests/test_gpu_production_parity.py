@@ -294,11 +294,10 @@ def test_config45_x3_blocks_teacher_forced(cfg45, name, lvl):
     B = 37 if H * W <= 16 else 3  # a ragged count of packed small patches
     g = torch.Generator().manual_seed(300 + lvl + 17 * len(name))
     worst = 0.0
-    # round 5: dx3 (packed tiles) wherever conv3_dx3.hip tiles the level -- config 4's 4x4 level
-    # (16 patches a tile, 64 / 128 outputs in groups of 4 fragments) and config 5's 27x23 level
-    # (bands of 16 patches); config 4's 2x2 level stays on wx3
-    want_dx3 = {("resflows_smallpatch_split", 0): 1, ("resflows_smallpatch_split", 1): 0,
-                ("resflow-patches-vqvae", 0): 1}[(name, lvl)]
+    # round 5: dx3 at every level -- config 4's 4x4 level (16 patches a tile in segments, 64 /
+    # 128 outputs in groups of 4 fragments), its 2x2 level and config 5's 27x23 level (gutter
+    # packing: patches at pitch W + 1 / H + 1 sharing one zero column / row)
+    want_dx3 = 1
     for bname, mod, db in _blocks(fl, eng, lvl):
         assert db.desc.wino and db.desc.wx3, (name, bname, "not on the split-f16 Winograd path")
         assert db.desc.dx3 == want_dx3, (name, lvl, bname, db.desc.dx3)
