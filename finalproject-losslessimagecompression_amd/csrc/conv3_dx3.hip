@@ -158,13 +158,6 @@ __device__ unsigned long long g_dx3_tl[4096][8];
 #else
 #define DX3_TL(j) do { } while (0)
 #endif
-// the waves that issue the DMA pieces: IDF_DX3_DMAW of them from wave IDF_DX3_DMAW0
-#ifndef IDF_DX3_DMAW
-#define IDF_DX3_DMAW IDF_DX3_WAVES
-#endif
-#ifndef IDF_DX3_DMAW0
-#define IDF_DX3_DMAW0 0
-#endif
 #ifndef IDF_DX3_KSPLIT
 #define IDF_DX3_KSPLIT 4  // chunks of the split-K levels (timing A/B builds only: changes bits)
 #endif
@@ -180,6 +173,10 @@ __device__ unsigned long long g_dx3_tl[4096][8];
 constexpr int kDxWaves = IDF_DX3_WAVES;
 constexpr int kDxThreads = 64 * kDxWaves;
 constexpr uint32_t kDxInvalid = 0xFFFFFFF0u;
+// slab-0 offset of an out-of-image halo slot: with the split buffer under 2 GiB (checked on the
+// host) kDxOff + s * slab stride lies past the buffer's end for every slab s, so the load
+// returns zeros
+constexpr uint32_t kDxOff = 0x80000000u;
 // the split-f16 range guard on stored outputs: |y| < 8192, as wx3 (|x| < 32768 on block inputs
 // is checked where the inputs are split, idf_dx3_split_cols)
 constexpr float kDxInGuard = 32768.0f;
@@ -206,8 +203,11 @@ struct Dx3Lds {
   static constexpr int FOFF = BOFF + 16 * NF * 16 * 4;  // the split-K "last block" flag
   static constexpr int BYTES = FOFF + 16;
   static constexpr int HPIECES = T * 2 * PLANE_KIB;        // halo DMA pieces per slab
-  static constexpr int NPIECES = HPIECES + WST / 1024;     // + weight pieces
-  static constexpr int PPW = (NPIECES + IDF_DX3_DMAW - 1) / IDF_DX3_DMAW;  // pieces per wave (max)
+  static constexpr int WPIECES = WST / 1024;               // weight pieces per slab
+  // piece slots per wave: halo slots [0, PH) then weight slots [PH, PPW); slot i of wave w is
+  // piece w + 8 i of its kind (some slots of the last row of each kind are empty)
+  static constexpr int PH = (HPIECES + kDxWaves - 1) / kDxWaves;
+  static constexpr int PPW = PH + (WPIECES + kDxWaves - 1) / kDxWaves;
 };
 
 typedef __attribute__((address_space(3))) void* dx_lds_ptr_t;
@@ -281,14 +281,24 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   const int64_t wbytes = (int64_t)g.nslab * wslab;
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)g.Wt, 0, (int)(wbytes < (int64_t)kDxInvalid ? wbytes : (int64_t)kDxInvalid), 0x00020000);
-  uint32_t pbase[L::PPW];  // per piece: source byte offset of slab 0 (halo) / within a slab (weights)
+  // Per slot: the source byte offset of slab 0 (halo: per lane; an out-of-image slot gets
+  // kDxOff, which stays past the buffer's end for every slab -- the buffer returns zeros, no
+  // select in the loop) or within a slab (weights); the LDS offset within a stage; whether the
+  // slot holds a piece (wave-uniform).  The kind of slot i is a compile-time fact, so a DMA in
+  // the loop is an address add, an M0 add and the load -- no per-piece branching.
+  uint32_t pbase[L::PPW];
+  int plo[L::PPW];
+  bool pok[L::PPW];
 #pragma unroll
   for (int i = 0; i < L::PPW; ++i) {
-    const int dw = wave - IDF_DX3_DMAW0;  // this wave's rank among the DMA-issuing waves
-    const int k = (dw >= 0 && dw < IDF_DX3_DMAW) ? dw + IDF_DX3_DMAW * i : (1 << 20);
-    pbase[i] = kDxInvalid;
-    if (k < L::HPIECES) {
+    const bool hk = i < L::PH;
+    const int k = wave + kDxWaves * (hk ? i : i - L::PH);
+    pok[i] = k < (hk ? L::HPIECES : L::WPIECES);
+    pbase[i] = kDxOff;
+    plo[i] = 0;
+    if (hk && pok[i]) {
       const int t = k / (2 * PLANE_KIB), pl = (k / PLANE_KIB) % 2, pi = k % PLANE_KIB;
+      plo[i] = (t * 2 + pl) * L::PLANE + pi * 1024;
       const int slot = 32 * pi + (lane >> 1);
       const int tt = tb * T + t;
       if (tt < g.ntiles) {
@@ -320,32 +330,24 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
         if (ok)
           pbase[i] = (uint32_t)(pl * plane_b + ((((int64_t)b * g.H + y) * g.Wd + x) * 32) + (lane & 1) * 16);
       }
-    } else if (k < L::NPIECES) {
-      pbase[i] = (uint32_t)(grp * L::WST + (k - L::HPIECES) * 1024 + lane * 16);
+    } else if (!hk && pok[i]) {
+      plo[i] = L::WOFF + k * 1024;
+      pbase[i] = (uint32_t)(grp * L::WST + k * 1024 + lane * 16);
     }
   }
-  // issue piece i of slab s into stage st
+  // issue slot i's piece of slab s into stage st (a slab past the layer's reads zeros: the
+  // loop's last slab issues its "next" DMA unconditionally, into a stage nothing reads again)
   auto dma = [&](int s, int st, int i) {
-    const int dw = wave - IDF_DX3_DMAW0;
-    const int k = (dw >= 0 && dw < IDF_DX3_DMAW) ? dw + IDF_DX3_DMAW * i : (1 << 20);
-    if (k >= L::NPIECES) return;
+    if (!pok[i]) return;
+    const bool halo = i < L::PH;
+    if (halo ? (IDF_DX3_ABLATE & 1) : (IDF_DX3_ABLATE & 4)) return;
     // one call site for both kinds of piece (the LDS address formed from the __shared__ array
     // itself): the host pass of hipcc drops the kernel's launch stub otherwise
-    const bool halo = k < L::HPIECES;
-    if (halo ? (IDF_DX3_ABLATE & 1) : (IDF_DX3_ABLATE & 4)) return;
-    int lo;
-    uint32_t off;
-    if (halo) {
-      const int t = k / (2 * PLANE_KIB), pl = (k / PLANE_KIB) % 2, pi = k % PLANE_KIB;
-      lo = (t * 2 + pl) * L::PLANE + pi * 1024;
-      off = pbase[i] == kDxInvalid ? kDxInvalid : pbase[i] + (uint32_t)s * xs_stride;
-    } else {
-      lo = L::WOFF + (k - L::HPIECES) * 1024;
-      off = pbase[i] + (uint32_t)(s * g.ngroup) * (uint32_t)L::WST;  // (a product of captured
-      // locals here left the lambda's captures in scratch: 144-160 B per lane)
-    }
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(halo ? xr : wr, (dx_lds_ptr_t)(lds + st * L::STAGE + lo),
-                                             16, off, 0, 0, 0);
+    const uint32_t off = pbase[i] + (halo ? (uint32_t)s * xs_stride
+                                          : (uint32_t)(s * g.ngroup) * (uint32_t)L::WST);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(halo ? xr : wr,
+                                             (dx_lds_ptr_t)(lds + st * L::STAGE + plo[i]), 16,
+                                             off, 0, 0, 0);
   };
 
   // zeros for the odd tap's pair, and the epilogue's bias table (both outside the stages)
@@ -863,8 +865,9 @@ extern "C" int idf_conv3x3_dx3(void* stream, int32_t B, int32_t H, int32_t W, in
   if ((uintptr_t)out % 16 || ld_out % 4) return IDF_ERR_ARG;  // 16-B output stores
   if ((C + 15) / 16 > nslab_xs) return IDF_ERR_ARG;          // the input slabs must exist
   const int64_t P = (int64_t)B * H * W;
-  // 32-bit buffer offsets: the split buffer must span < 4 GiB
-  if (idf_dx3_split_bytes(P, 16 * nslab_xs) >= (int64_t)kDxInvalid) return IDF_ERR_UNSUPPORTED;
+  // 32-bit buffer offsets, and kDxOff past the end of every slab: the split buffer must span
+  // < 2 GiB (imagenet64's 32x32 level: B < ~960 images)
+  if (idf_dx3_split_bytes(P, 16 * nslab_xs) >= (int64_t)kDxOff) return IDF_ERR_UNSUPPORTED;
   const int64_t nblk = (int64_t)sh.nblk_tiles * sh.pl.ngroup * sh.nchunk;
   if (sh.ntiles >= (1 << 20) || nblk >= (1 << 20)) return IDF_ERR_UNSUPPORTED;  // udiv_s operands
   Dx3Args g = {};
