@@ -47,6 +47,7 @@
 
 #include <utility>
 
+#include "idf_cdf.h"
 #include "idf_codec_internal.h"
 #include "wino_common.h"
 
@@ -89,6 +90,16 @@ struct Dx3Args {
   int64_t ldo;
   float yscale;
   uint32_t* flag;  // bit 0: range guard tripped
+  // the DenseBlock head fused into the layer (IdfDx3Head; nh = 0: none)
+  const float* hw;      // [nh][ldhw] fp32 head weights (padded channel coordinates)
+  int32_t ldhw, nh;
+  float* hacc;          // [P][16] running head sums
+  int32_t hlast, skip_f32, hmode, hn_mean;
+  float* hout;
+  int64_t hld_out;
+  const float* hbase;
+  int64_t hld_base;
+  float *hmean, *hlogs, *hscale;
 };
 
 // timing-only ablations (tools/dx3_build_ablate.sh builds; never set in the library build):
@@ -200,7 +211,8 @@ struct Dx3Lds {
   static constexpr int STAGE = WOFF + WST;
   static constexpr int ZOFF = 2 * STAGE;           // NF * 512 B of zeros (the odd tap's pair)
   static constexpr int BOFF = ZOFF + NF * 512;     // bias table [16 classes][NF * 16] f32
-  static constexpr int FOFF = BOFF + 16 * NF * 16 * 4;  // the split-K "last block" flag
+  static constexpr int HOFF = BOFF + 16 * NF * 16 * 4;  // fused head weights [16][NF * 16] f32
+  static constexpr int FOFF = HOFF + 16 * NF * 16 * 4;  // the split-K "last block" flag
   static constexpr int BYTES = FOFF + 16;
   static constexpr int HPIECES = T * 2 * PLANE_KIB;        // halo DMA pieces per slab
   static constexpr int WPIECES = WST / 1024;               // weight pieces per slab
@@ -363,6 +375,14 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   DX3_PHASE(4, __builtin_amdgcn_s_memrealtime());
   stage_bias((float*)(lds + L::BOFF), NF * 16, grp * NF * 16, g.N, g.b3, g.vtap, g.bfull, g.ldv,
              tid, kDxThreads);
+  if (g.nh > 0) {  // the head's weights on this layer's output channels ([16][NF * 16], zeros
+                   // past nh and past the layer's N outputs)
+    float* htab = (float*)(lds + L::HOFF);
+    for (int e = tid; e < 16 * NF * 16; e += kDxThreads) {
+      const int o = e / (NF * 16), cc = e - o * (NF * 16), col = grp * NF * 16 + cc;
+      htab[e] = (o < g.nh && col < g.N) ? g.hw[(int64_t)o * g.ldhw + g.C + col] : 0.0f;
+    }
+  }
   DX3_PHASE(1, __builtin_amdgcn_s_memtime());
   DX3_TL(1);
 
@@ -595,14 +615,18 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   }
 
   // ---- epilogue: lane holds outputs 16 (grp NF + n) + 4q .. +3 of packed pixel (row r0 + m,
-  // column j) of its tile.  fp32 outputs to out; their split pairs to XS at channel C + that
-  // output (zeros for the padding outputs >= N and -- the last group -- on to the next
-  // 16-channel boundary past C + N, so the next layer's last slab reads finite values; never
-  // past the split buffer).
+  // column j) of its tile.  fp32 outputs to out (unless skip_f32); their split pairs to XS at
+  // channel C + that output (zeros for the padding outputs >= N and -- the last group -- on to
+  // the next 16-channel boundary past C + N, so the next layer's last slab reads finite values;
+  // never past the split buffer).  With a fused head every lane of the wave takes part in the
+  // head's cross-lane sums, so lanes without an output (gutter columns, rows past the image,
+  // images past the batch) compute and only skip their stores.
   if (tile >= g.ntiles) return;
-  if (xj >= g.Wd || ixj >= g.nbx) return;  // a gutter column or past the band (gutter packing)
+  const bool lane_ok = xj < g.Wd && ixj < g.nbx;  // a gutter column or past the band: no output
   const WAct act(g.act, g.slope);
   const float* btab = (const float*)(lds + L::BOFF);
+  const float* htab = (const float*)(lds + L::HOFF);
+  const bool fh = g.nh > 0;
   bool out_ok = true;
   const int zr = (g.C + g.N + 15) / 16 * 16, zend = zr < 16 * g.nslab_xs ? zr : 16 * g.nslab_xs;
   const bool lastg = grp == g.ngroup - 1;
@@ -615,10 +639,14 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
       y = uyw + m - iy * g.hp;
     }
     const int b_img = (dt.band * g.nby + iy) * g.nbx + ixj;
-    if (y >= g.H || iy >= g.nby || b_img >= g.B) continue;
+    const bool row_ok = lane_ok && y < g.H && iy < g.nby && b_img < g.B;
+    if (!row_ok && !fh) continue;
     const int cls = bias_class(y, xj, g.H, g.Wd);
     const int64_t pix = ((int64_t)b_img * g.H + y) * g.Wd + xj;
     float* dst = g.out + pix * g.ldo;
+    float hp[16];  // this lane's share of the head sums of its pixel (its 4 x NF channels)
+#pragma unroll
+    for (int o = 0; o < 16; ++o) hp[o] = 0.0f;
 #pragma unroll
     for (int n = 0; n <= NF; ++n) {
       if (n == NF && !lastg) break;
@@ -631,24 +659,85 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
         for (int k = 0; k < 4; ++k) {
           const float t = acc[m][n][k] * g.yscale + bv[k];
           v[k] = act.tanh_ ? wact(t, g.act, g.slope) : act(t);
-          out_ok = out_ok && fabsf(v[k]) < kDxOutGuard;
+          if (row_ok) out_ok = out_ok && fabsf(v[k]) < kDxOutGuard;
         }
-        if (n0 + 4 <= g.N) {
-          *(d4*)(dst + n0) = v;
-        } else {
+        if (row_ok && !g.skip_f32) {
+          if (n0 + 4 <= g.N) {
+            *(d4*)(dst + n0) = v;
+          } else {
 #pragma unroll
-          for (int k = 0; k < 4; ++k)
-            if (n0 + k < g.N) dst[n0 + k] = v[k];
-          for (int k = g.N - n0; k < 4; ++k) v[k] = 0.0f;
+            for (int k = 0; k < 4; ++k)
+              if (n0 + k < g.N) dst[n0 + k] = v[k];
+          }
+        }
+        for (int k = g.N - n0; k < 4; ++k) v[k] = 0.0f;
+        if (fh) {  // head share: channels in order, fragments in order (zero weights past N)
+#pragma unroll
+          for (int o = 0; o < 16; ++o) {
+            if (o >= g.nh) break;
+            const d4 wv = *(const d4*)(htab + o * (NF * 16) + nl);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) hp[o] = __builtin_fmaf(wv[k], v[k], hp[o]);
+          }
         }
       }
       const int c = g.C + n0;  // split channel of v[0]; c % 4 == 0, so v stays in one slab
-      if (!(IDF_DX3_ABLATE & 128) && c < zend) {
+      if (row_ok && !(IDF_DX3_ABLATE & 128) && c < zend) {
         const e4 h = __builtin_convertvector(v, e4);
         const e4 l = __builtin_convertvector(v - __builtin_convertvector(h, d4), e4);
         char* p = xsb + (int64_t)(c >> 4) * 2 * plane_b + pix * 32 + (c & 15) * 2;
         *(e4*)p = h;
         *(e4*)(p + plane_b) = l;
+      }
+    }
+    if (fh) {
+      // the pixel's 4 lanes (q) reduce-scatter their shares: lane q ends with the sums of head
+      // outputs 4q .. 4q + 3 -- (h_q + h_q^2) then + the pair q^1 -- one fixed order per output
+      float r8[8], r4[4];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float mine = q < 2 ? hp[i] : hp[8 + i];
+        const float give = q < 2 ? hp[8 + i] : hp[i];
+        r8[i] = mine + __shfl_xor(give, 32);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float mine = (q & 1) ? r8[4 + i] : r8[i];
+        const float give = (q & 1) ? r8[i] : r8[4 + i];
+        r4[i] = mine + __shfl_xor(give, 16);
+      }
+      if (row_ok && 4 * q < g.nh) {
+        d4* ap = (d4*)(g.hacc + pix * 16 + 4 * q);
+        const d4 prev = *ap;
+        d4 hv;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) hv[i] = prev[i] + r4[i];
+        if (!g.hlast) {
+          *ap = hv;
+        } else {  // the complete head: its epilogue (flow_kernels.hip gemm_f32_kernel's)
+          const int64_t hw_ = (int64_t)g.H * g.Wd, rem = (int64_t)y * g.Wd + xj;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int o = 4 * q + i;
+            if (o >= g.nh) break;
+            const float vv = hv[i];
+            if (g.hmode == IDF_EPI_COUPLE_ADD || g.hmode == IDF_EPI_COUPLE_SUB) {
+              const float r = __builtin_rintf(vv * 256.0f) / 256.0f;  // roundlib.py:34-38
+              const float bsv = g.hbase[pix * g.hld_base + o];
+              g.hout[pix * g.hld_out + o] = g.hmode == IDF_EPI_COUPLE_ADD ? bsv + r : bsv - r;
+            } else if (g.hmode == IDF_EPI_PRIOR) {
+              if (o < g.hn_mean) {
+                g.hmean[((int64_t)b_img * g.hn_mean + o) * hw_ + rem] = vv;
+              } else {
+                const int64_t oi = ((int64_t)b_img * g.hn_mean + (o - g.hn_mean)) * hw_ + rem;
+                g.hlogs[oi] = vv;
+                g.hscale[oi] = expf_glibc(vv);
+              }
+            } else {
+              g.hout[pix * g.hld_out + o] = vv;
+            }
+          }
+        }
       }
     }
   }
@@ -849,12 +938,58 @@ extern "C" int idf_dx3_split_cols(void* stream, int64_t P, int32_t c0, int32_t c
   return idf_last_error();
 }
 
+// The fused head's running sums start from the block input: acc[p][o] = bias[o] + sum over
+// c < C0 of w[o][c] x[p][c] (c in order), o < n_head; 0 for n_head <= o < 16.  One thread per
+// pixel, scalar FMAs on the weights read from global memory (wave-uniform, cached).  A version
+// staging the weights in LDS (packed FMAs on broadcast ds_read_b128) returned different sums for
+// runs of 16 pixels when it ran beside another stream's dx3 layers on the same CUs -- the table
+// itself checked intact before and after -- so two decode lanes diverged (profiles/r05/
+// fused_head/lds_coresidency.txt; tests/test_gpu_lanes.py test_fused_blocks_two_streams).
+__global__ void __launch_bounds__(256) dx3_head_init_kernel(int64_t P, int32_t C0,
+                                                            const float* __restrict__ x,
+                                                            int64_t ld_x, const float* __restrict__ w,
+                                                            int32_t ldw, const float* __restrict__ bias,
+                                                            int32_t nh, float* __restrict__ acc) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  float h[16];
+#pragma unroll
+  for (int o = 0; o < 16; ++o) h[o] = o < nh ? bias[o] : 0.0f;
+  const float* xr = x + p * ld_x;
+  for (int c = 0; c < C0; c += 4) {
+    const d4 xv = *(const d4*)(xr + c);
+#pragma unroll
+    for (int o = 0; o < 16; ++o) {
+      if (o >= nh) break;
+      const d4 wv = *(const d4*)(w + (int64_t)o * ldw + c);  // uniform: one scalar 16-B load
+#pragma unroll
+      for (int k = 0; k < 4; ++k) h[o] = __builtin_fmaf(wv[k], xv[k], h[o]);
+    }
+  }
+  d4* ap = (d4*)(acc + p * 16);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ap[i] = d4{h[4 * i], h[4 * i + 1], h[4 * i + 2], h[4 * i + 3]};
+}
+
+extern "C" int idf_dx3_head_init(void* stream, int64_t P, int32_t C0, const float* x, int64_t ld_x,
+                                 const float* w, int32_t ldw, const float* bias, int32_t n_head,
+                                 float* acc) {
+  if (P <= 0) return P < 0 ? IDF_ERR_ARG : IDF_OK;
+  if (!x || !w || !bias || !acc || n_head < 1 || n_head > 16 || C0 < 0 || C0 > 64 || (C0 & 3) ||
+      (ld_x & 3) || (uintptr_t)x % 16 || (uintptr_t)acc % 16 || ldw < C0 || (ldw & 3) ||
+      (uintptr_t)w % 16)
+    return IDF_ERR_ARG;
+  hipLaunchKernelGGL(dx3_head_init_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, P, C0, x, ld_x, w, ldw, bias, n_head, acc);
+  return idf_last_error();
+}
+
 extern "C" int idf_conv3x3_dx3(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
                                uint16_t* xs, int32_t nslab_xs, const uint16_t* w, int32_t nft,
                                float yscale, const float* b3, const float* vtap, int32_t ldv,
                                const float* bfull, int32_t N, float* out, int64_t ld_out,
                                int32_t act, float slope, uint32_t* d_flag, void* d_workspace,
-                               int64_t workspace_bytes) {
+                               int64_t workspace_bytes, const IdfDx3Head* head) {
   if (B <= 0 || H <= 0 || W <= 0 || N <= 0) return IDF_OK;
   if (C <= 0 || (C & 3) || !w || !xs || !out || !b3) return IDF_ERR_ARG;
   const Dx3Launch sh = dx3_launch_shape(B, H, W, C, N);
@@ -891,6 +1026,26 @@ extern "C" int idf_conv3x3_dx3(void* stream, int32_t B, int32_t H, int32_t W, in
   g.nchunk = sh.nchunk; g.chunk_slabs = sh.chunk_slabs;
   g.b3 = b3; g.vtap = vtap; g.bfull = bfull; g.ldv = ldv; g.act = act; g.slope = slope;
   g.out = out; g.ldo = ld_out; g.yscale = yscale; g.flag = d_flag;
+  if (head && head->n_head > 0) {
+    // one block writes a pixel's running head sums: one output group only; <= 16 outputs
+    if (head->n_head > 16 || sh.pl.ngroup != 1 || !head->w || !head->acc || head->ldw < C + N ||
+        (uintptr_t)head->acc % 16)
+      return IDF_ERR_ARG;
+    const IdfHeadOut& o = head->out;
+    if (head->last) {
+      if (o.mode == IDF_EPI_PRIOR ? (!o.mean || !o.logscale || !o.scale || o.n_mean < 0 ||
+                                     2 * o.n_mean != head->n_head)
+                                  : (!o.out || ((o.mode == IDF_EPI_COUPLE_ADD ||
+                                                 o.mode == IDF_EPI_COUPLE_SUB) && !o.base)))
+        return IDF_ERR_ARG;
+    }
+    g.hw = head->w; g.ldhw = head->ldw; g.nh = head->n_head; g.hacc = head->acc;
+    g.hlast = head->last; g.skip_f32 = head->skip_f32; g.hmode = o.mode; g.hn_mean = o.n_mean;
+    g.hout = o.out; g.hld_out = o.ld_out; g.hbase = o.base; g.hld_base = o.ld_base;
+    g.hmean = o.mean; g.hlogs = o.logscale; g.hscale = o.scale;
+  } else if (head && head->skip_f32) {
+    g.skip_f32 = 1;
+  }
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)nblk), blk(kDxThreads);
 #define IDF_DX3_GO(nf_, wr_, pitch_, kib_) \

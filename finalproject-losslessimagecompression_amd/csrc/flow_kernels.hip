@@ -639,6 +639,7 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
   int32_t nslab_xs = 0;
   char* dws = nullptr;  // the dx3 layers' split-K counters and partial sums, after the copy
   int64_t dws_bytes = 0;
+  float* hacc = nullptr;  // the fused head's running sums (nullptr: the head GEMM runs)
   const int dx3_nft = [&] {  // fragments the dx3 weights hold (packing.dx3_groups)
     const int nft = (blk->g_pad + 15) / 16, nf = nft < 4 ? nft : 4;
     return (nft + nf - 1) / nf * nf;
@@ -654,15 +655,35 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
     if (need < 0 || off + need > avail || (uintptr_t)tmp % 256) return IDF_ERR_WORKSPACE;
     xs = (uint16_t*)tmp;
     dws = (char*)tmp + off;
-    dws_bytes = avail - off;
+    dws_bytes = need;
+    // the fused head (IdfDenseBlock.fuse_head): every layer on dx3 in one output group, a
+    // head of <= 16 outputs over a block input of <= 64 channels; its running sums [P][16]
+    // after the split-K workspace
+    if (head && blk->fuse_head && n_dx3 == blk->depth && blk->n_head <= 16 && dx3_nft <= 4 &&
+        blk->k_in[0] <= 64 && blk->depth > 0) {
+      const int64_t hoff = (off + need + 255) / 256 * 256;
+      if (hoff + P * 64 <= avail) hacc = (float*)((char*)tmp + hoff);
+    }
     const int64_t ctr = idf_conv3x3_dx3_counter_bytes(B, H, W, blk->g_pad);
     int rc = idf_dx3_split_cols(stream, P, 0, blk->k_in[0], feat, ld_feat, xs, nslab_xs,
                                 blk->range_flag, need > 0 ? (uint32_t*)dws : nullptr,
                                 need > 0 ? (int32_t)(ctr / 4) : 0);
     if (rc) return rc;
+    if (hacc) {
+      rc = idf_dx3_head_init(stream, P, blk->k_in[0], feat, ld_feat, blk->wh, blk->ldwh, blk->bh,
+                             blk->n_head, hacc);
+      if (rc) return rc;
+    }
   }
   for (int i = 0; i < blk->depth; ++i) {
     const int c = blk->k_in[i];
+    IdfDx3Head hd = {};
+    if (hacc) {
+      hd.w = blk->wh; hd.ldw = blk->ldwh; hd.n_head = blk->n_head; hd.acc = hacc;
+      hd.last = i == blk->depth - 1;
+      hd.skip_f32 = blk->keep_feat ? 0 : 1;
+      hd.out = *head;
+    }
     const double cr = blk->c_real[i], gr = blk->g_real[i];
     if (blk->fold) {  // one launch per layer: 3x3 over the layer input, 1x1 folded in
       timer_mark(timer, s, IDF_TAG_CONV3X3, 2.0 * P * 9.0 * cr * gr, true);
@@ -678,7 +699,8 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
                    ? idf_conv3x3_dx3(stream, B, H, W, c, xs, nslab_xs, blk->dx3_w[i], dx3_nft,
                                      blk->dx3_yscale[i], blk->b3[i], blk->vtap[i], blk->ldv,
                                      blk->bfull[i], blk->g_pad, feat + c, ld_feat, blk->act,
-                                     blk->slope, blk->range_flag, dws, dws_bytes)
+                                     blk->slope, blk->range_flag, dws, dws_bytes,
+                                     hacc ? &hd : nullptr)
                : (wino && blk->wx3 && blk->wx3_u[i])
                    ? idf_conv3x3_wx3(stream, B, H, W, c, feat, ld_feat, blk->wx3_u[i],
                                      blk->wino_nft, blk->wx3_yscale[i], blk->b3[i], blk->vtap[i],
@@ -715,7 +737,7 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
     timer_mark(timer, s, 0, 0, false);
     if (rc) return rc;
   }
-  if (!head) return IDF_OK;  // caller runs the head itself
+  if (!head || hacc) return IDF_OK;  // caller runs the head itself / fused into the last layer
   timer_mark(timer, s, IDF_TAG_HEAD, 2.0 * P * blk->c_real[blk->depth] * blk->n_head, true);
   int rc = idf_conv1x1_f32(stream, P, blk->k_in[blk->depth], blk->n_head, feat, ld_feat, blk->wh,
                            blk->ldwh, blk->nh_alloc, blk->bh, nullptr, 0, B, H, W, head);

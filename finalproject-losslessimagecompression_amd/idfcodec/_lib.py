@@ -56,6 +56,7 @@ class IdfDenseBlock(ctypes.Structure):
         ("bf16", i32), ("wb16", P * MAX_DEPTH),
         ("wx3", i32), ("wx3_yscale", f32 * MAX_DEPTH), ("wx3_u", P * MAX_DEPTH), ("range_flag", P),
         ("dx3", i32), ("dx3_yscale", f32 * MAX_DEPTH), ("dx3_w", P * MAX_DEPTH),
+        ("fuse_head", i32), ("keep_feat", i32),
     ]
 
 
@@ -63,6 +64,13 @@ class IdfHeadOut(ctypes.Structure):
     _fields_ = [
         ("mode", i32), ("out", P), ("ld_out", i64), ("base", P), ("ld_base", i64),
         ("n_mean", i32), ("mean", P), ("logscale", P), ("scale", P),
+    ]
+
+
+class IdfDx3Head(ctypes.Structure):
+    _fields_ = [
+        ("w", P), ("ldw", i32), ("n_head", i32), ("acc", P), ("last", i32), ("skip_f32", i32),
+        ("out", IdfHeadOut),
     ]
 
 
@@ -113,7 +121,8 @@ SIGNATURES = {
                                            i64, P, i64, i32, f32, P, i32, P, i64]),
     "idf_conv3x3_dx3_supported": (ctypes.c_int, [i32, i32, i32]),
     "idf_conv3x3_dx3": (ctypes.c_int, [P, i32, i32, i32, i32, P, i32, P, i32, f32, P, P, i32, P,
-                                       i32, P, i64, i32, f32, P, P, i64]),
+                                       i32, P, i64, i32, f32, P, P, i64, P]),
+    "idf_dx3_head_init": (ctypes.c_int, [P, i64, i32, P, i64, P, i32, P, i32, P]),
     "idf_conv3x3_dx3_counter_bytes": (i64, [i32, i32, i32, i32]),
     "idf_conv3x3_dx3_workspace": (i64, [i32, i32, i32, i32, i32]),
     "idf_dx3_split_bytes": (i64, [i64, i32]),

@@ -52,6 +52,14 @@ WX3 = os.environ.get("IDF_WX3", "1") != "0"
 # 16 on dx3 -- decodes version-2 files with conv code 6), 'x3', 'f32'; the mode is recorded in
 # the bitstream.
 DX3 = os.environ.get("IDF_DX3", "1") != "0"
+# In 'dx3' mode a DenseBlock whose layers all run on dx3 (one output group) with a head of <= 16
+# outputs (every coupling, the 32x32 prior) fuses the head into its layers: running sums from
+# the block input (idf_dx3_head_init), each layer's epilogue adds its outputs' share, the last
+# applies the coupling / prior epilogue -- no head GEMM re-reading the feature buffer, and the
+# layers skip their fp32 output stores (IdfDenseBlock.fuse_head / keep_feat).  IDF_HEAD_FUSE=0
+# keeps the GEMM heads (timing A/B only: the head's sums run in another order, so encoder and
+# decoder must agree on it).
+HEAD_FUSE = os.environ.get("IDF_HEAD_FUSE", "1") != "0"
 
 
 class DeviceBlock:
@@ -112,6 +120,8 @@ class DeviceBlock:
             d.wx3_u[i] = u.data_ptr()
             d.wx3_yscale[i] = packed.wx3_yscale[i]
         d.dx3 = 1 if (d.wx3 and self.dx3_w) else 0
+        d.fuse_head = 1 if (d.dx3 and HEAD_FUSE) else 0
+        d.keep_feat = 0
         for i, w in enumerate(self.dx3_w):
             d.dx3_w[i] = w.data_ptr()
             d.dx3_yscale[i] = packed.dx3_yscale[i]
@@ -323,6 +333,8 @@ class FlowEngine:
             for b in self.couple[l] + [self.prior[l]]:
                 b.desc.wx3 = on if b.wx3_u else 0
                 b.desc.dx3 = 1 if (dl and b.dx3_w and b.desc.wx3) else 0
+                # round 5's dx3 fuses the heads; dx3w16 (round 4's arithmetic) keeps the GEMMs
+                b.desc.fuse_head = 1 if (mode == "dx3" and b.desc.dx3 and HEAD_FUSE) else 0
         self.conv_mode = mode  # each mode's top prior is cached separately (_top_prior)
 
     @property
@@ -413,7 +425,8 @@ class FlowEngine:
                     w = lib().idf_conv3x3_dx3_workspace(B, Lv.h, Lv.w, b.geom.k_in[nd - 1],
                                                         b.geom.g_pad)
                     extra = max(extra, int(w))
-            n = max(n, P * self.ld_tmp + ((extra + 256) // 4 + 16 * P if extra > 0 else 0))
+            # + the fused head's running sums [P][16] (and the split-K workspace)
+            n = max(n, P * self.ld_tmp + (extra + 512) // 4 + 32 * P)
         return n
 
     def tmp_pitch(self, ws, P: int) -> int:

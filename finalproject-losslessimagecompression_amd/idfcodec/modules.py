@@ -12,7 +12,7 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import check, lib, ptr, require_device
+from ._lib import IdfHeadOut, check, lib, ptr, require_device
 from .engine import FLOAT, DeviceBlock, head_couple, head_prior
 from .packing import pack_dense_block, round_up
 
@@ -68,10 +68,9 @@ def dense_tmp(db: DeviceBlock, B: int, H: int, W: int, ld_tmp: int, device):
     P = B * H * W
     n = P * ld_tmp
     nd = len(db.dx3_w)
-    if nd and db.desc.dx3:
+    if nd and db.desc.dx3:  # + the split-K workspace and the fused head's sums [P][16]
         w = int(lib().idf_conv3x3_dx3_workspace(B, H, W, db.geom.k_in[nd - 1], db.geom.g_pad))
-        if w > 0:
-            n += (w + 256) // 4 + 16 * P
+        n += (max(w, 0) + 512) // 4 + 32 * P
     tmp = torch.empty(n, dtype=torch.float32, device=device)
     return tmp, max(ld_tmp, (n // P) // 16 * 16)
 
@@ -100,12 +99,20 @@ def run_device_block(db: DeviceBlock, x: torch.Tensor, return_feat: bool = False
     n = db.geom.n_head
     ldo = round_up(n, 4)
     out_pm = torch.empty(B * H * W * ldo, dtype=torch.float32, device=x.device)
-    check(lib().idf_dense_block_f32(s, ctypes.byref(db.desc), B, H, W, ptr(feat), ld,
-                                    ptr(tmp), ld_tmp, None), "dense block")
-    # head=NULL skips the head inside the block call; run it with a plain store epilogue
-    check(lib().idf_conv1x1_f32(s, B * H * W, db.geom.width, n, ptr(feat), ld, ptr(db.wh),
-                                db.packed.ldwh, db.packed.nh_alloc, ptr(db.bh), ptr(out_pm), ldo, B,
-                                H, W, None), "head")
+    # the head inside the block call with a plain store epilogue -- fused into the dx3 layers
+    # where the engine fuses it, else the head GEMM -- and, for return_feat, the layers' fp32
+    # outputs kept (a fused head otherwise drops them)
+    head = IdfHeadOut()
+    head.mode = _lib.EPI_STORE
+    head.out = ptr(out_pm)
+    head.ld_out = ldo
+    keep = db.desc.keep_feat
+    db.desc.keep_feat = 1 if return_feat else keep
+    try:
+        check(lib().idf_dense_block_f32(s, ctypes.byref(db.desc), B, H, W, ptr(feat), ld,
+                                        ptr(tmp), ld_tmp, ctypes.byref(head)), "dense block")
+    finally:
+        db.desc.keep_feat = keep
     out = torch.empty((B, n, H, W), dtype=torch.float32, device=x.device)
     check(lib().idf_pm_to_nchw(s, B, n, H, W, ptr(out_pm), ldo, ptr(out)), "pm_to_nchw")
     return out, (feat.view(P, ld) if return_feat else None)

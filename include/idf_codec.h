@@ -204,6 +204,15 @@ typedef struct IdfDenseBlock {
   int32_t dx3;
   float dx3_yscale[IDF_MAX_DEPTH];
   const uint16_t *dx3_w[IDF_MAX_DEPTH];
+  /* fuse_head = 1: when every layer runs on dx3 (with one output group) and n_head <= 16, the
+   * 1x1 head (nnblock.py:48-51) is not a separate GEMM over the whole feature buffer: its sums
+   * start from the block input (idf_dx3_head_init) and every dx3 layer's epilogue adds its own
+   * outputs' share (IdfDx3Head); the last layer applies the head epilogue.  keep_feat = 0 then
+   * also drops the layers' fp32 output stores (only the split copy is read); 1 keeps them (the
+   * per-layer parity tests read the fp32 features).  The head's sums run in another order than
+   * the GEMM's, so the flag is part of the conv arithmetic an encoder and its decoder share. */
+  int32_t fuse_head;
+  int32_t keep_feat;
 } IdfDenseBlock;
 
 /* Head epilogue target */
@@ -365,11 +374,32 @@ int64_t idf_conv3x3_dx3_workspace(int32_t B, int32_t H, int32_t W, int32_t C, in
 int idf_dx3_split_cols(void *stream, int64_t P, int32_t c0, int32_t c1, const float *d_x,
                        int64_t ld_x, uint16_t *d_xs, int32_t nslab_xs, uint32_t *d_flag,
                        uint32_t *d_zero, int32_t nzero);
+/* The DenseBlock head fused into its dx3 layers (IdfDenseBlock.fuse_head): per pixel a running
+ * fp32 sum d_acc [P][16] of the head's n_head <= 16 outputs.  idf_dx3_head_init starts it:
+ * d_acc[p][o] = bias[o] + sum_{c < C0} w[o][c] x[p][c] (c in order; o >= n_head: 0), from the
+ * block input's fp32 columns.  Each dx3 layer given an IdfDx3Head adds its outputs' share
+ * (per lane 4 channels x fragments in order, then the 4 lanes of a pixel pairwise) and, with
+ * last = 1, applies `out` to the complete sums: IDF_EPI_STORE (out.out[p][o]), COUPLE_ADD /
+ * COUPLE_SUB (the round-to-1/256 coupling, couplelib.py:47-61) or PRIOR (NCHW mean / logscale /
+ * scale = expf, priorlib.py:36-47).  skip_f32 = 1 drops the layer's fp32 output stores. */
+typedef struct IdfDx3Head {
+  const float *w;        /* [n_head][ldw] fp32, the padded channel coordinates of feat     */
+  int32_t ldw;
+  int32_t n_head;
+  float *acc;            /* [P][16]                                                         */
+  int32_t last;
+  int32_t skip_f32;
+  IdfHeadOut out;
+} IdfDx3Head;
+int idf_dx3_head_init(void *stream, int64_t P, int32_t C0, const float *d_x, int64_t ld_x,
+                      const float *d_w, int32_t ldw, const float *d_bias, int32_t n_head,
+                      float *d_acc);
 int idf_conv3x3_dx3(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, uint16_t *d_xs,
                     int32_t nslab_xs, const uint16_t *d_w, int32_t nft, float yscale,
                     const float *d_b3, const float *d_vtap, int32_t ldv, const float *d_bfull,
                     int32_t N, float *d_out, int64_t ld_out, int32_t act, float slope,
-                    uint32_t *d_flag, void *d_workspace, int64_t workspace_bytes);
+                    uint32_t *d_flag, void *d_workspace, int64_t workspace_bytes,
+                    const IdfDx3Head *head);
 
 /* The same folded 3x3 conv on bf16 MFMA (v_mfma_f32_16x16x32_bf16, fp32 accumulation).
  * The input is the bf16 shadow d_x16 of the fp32 feature columns (ld_x16 a multiple of 8,

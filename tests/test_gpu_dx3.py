@@ -111,14 +111,14 @@ def run_dx3(cs, act, X=None, B=None, layer2=False):
     if not layer2:
         check(lib().idf_conv3x3_dx3(s, B, H, W, C, ptr(xs), nslab, ptr(Wdd), nft, ysc,
                                     ptr(b3d), ptr(vtd), n_alloc, ptr(bfd), N, ptr(out), ld,
-                                    _lib.ACT[act], 0.01, ptr(flag), ptr(ws), wsb), "dx3")
+                                    _lib.ACT[act], 0.01, ptr(flag), ptr(ws), wsb, None), "dx3")
         torch.cuda.synchronize()
         counters_zero()
         return out.cpu(), int(flag.item()), xs.cpu(), P, nslab
     # layer 1 writes its fp32 outputs into X[:, C:C+N] and the split ones into xs
     check(lib().idf_conv3x3_dx3(s, B, H, W, C, ptr(xs), nslab, ptr(Wdd), nft, ysc,
                                 ptr(b3d), ptr(vtd), n_alloc, ptr(bfd), N, ptr(Xd) + 4 * C, ld,
-                                _lib.ACT[act], 0.01, ptr(flag), ptr(ws), wsb), "dx3 layer 1")
+                                _lib.ACT[act], 0.01, ptr(flag), ptr(ws), wsb, None), "dx3 layer 1")
     counters_zero()
     C2 = C + N
     W2 = torch.from_numpy(np.random.default_rng(C2).normal(0, 1 / np.sqrt(9 * C2), (n_alloc, 9, C2)))
@@ -127,7 +127,7 @@ def run_dx3(cs, act, X=None, B=None, layer2=False):
     Wdd2 = torch.from_numpy(Wd2.view(np.int16)).to(dev)
     check(lib().idf_conv3x3_dx3(s, B, H, W, C2, ptr(xs), nslab, ptr(Wdd2), nft, ysc2,
                                 ptr(b3d), ptr(vtd), n_alloc, ptr(bfd), N, ptr(out), ld,
-                                _lib.ACT[act], 0.01, ptr(flag), ptr(ws), wsb), "dx3 layer 2")
+                                _lib.ACT[act], 0.01, ptr(flag), ptr(ws), wsb, None), "dx3 layer 2")
     torch.cuda.synchronize()
     counters_zero()
     return out.cpu(), int(flag.item()), xs.cpu(), P, nslab, Xd.cpu(), W2
@@ -334,3 +334,108 @@ def test_dx3_packed_batch_invariant():
             one = cs["X"][i * P: (i + 1) * P].clone()
             alone = run_dx3(cs, "LeakyReLU", X=one, B=1)[0]
             assert torch.equal(full[i * P: (i + 1) * P], alone), (H, W, i)
+
+
+@pytest.mark.parametrize("B,H,W,nh,N", [(2, 32, 32, 3, 44), (3, 16, 16, 12, 44), (5, 8, 8, 16, 44),
+                                        (3, 27, 23, 6, 44), (40, 2, 2, 12, 44), (37, 4, 4, 6, 64),
+                                        (150, 2, 2, 12, 64), (9, 27, 23, 6, 64)])
+def test_dx3_fused_head(B, H, W, nh, N):
+    """The DenseBlock head fused into two dx3 layers (IdfDx3Head): running sums from the block
+    input (idf_dx3_head_init), each layer's share, the last layer's epilogue -- STORE within 1e-5
+    of an fp64 head over the kernels' own features; the fp32 stores skipped without changing a
+    bit; COUPLE_ADD / COUPLE_SUB exact inverses that round the same sums; PRIOR = the sums as
+    NCHW mean / logscale and exp(logscale); an image's head the same bits alone or inside a
+    batch (the decoder runs other batch compositions than the encoder)."""
+    from idfcodec import _lib
+    from idfcodec._lib import IdfDx3Head, check, lib, ptr
+    from idfcodec.packing import dx3_groups, dx3_weights
+    import ctypes
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(B * 31 + nh)
+    C0 = 20
+    C1, C2 = C0 + N, C0 + 2 * N
+    P = B * H * W
+    n_alloc = (N + 15) // 16 * 16
+    nf, ngroup = dx3_groups(n_alloc)
+    ld = (C2 + 15) // 16 * 16 + 16
+    X = torch.zeros(P, ld)
+    X[:, :C0] = torch.randn(P, C0, generator=g)
+    Xd = X.to(dev)
+    Ws = [torch.randn(n_alloc, 9, (c + 15) // 16 * 16, generator=g, dtype=torch.float64) / np.sqrt(9 * c)
+          for c in (C0, C1)]
+    for w, c in zip(Ws, (C0, C1)):
+        w[N:] = 0.0
+        w[:, :, c:] = 0.0
+    packs = [dx3_weights(w.numpy(), c) for w, c in zip(Ws, (C0, C1))]
+    wdev = [torch.from_numpy(wd.view(np.int16)).to(dev) for wd, _ in packs]
+    b3 = (torch.randn(n_alloc, generator=g) * 0.1).to(dev)
+    ldwh = (C2 + 15) // 16 * 16
+    wh = torch.zeros(nh, ldwh)
+    wh[:, :C2] = torch.randn(nh, C2, generator=g) / np.sqrt(C2)
+    bh = torch.randn(nh, generator=g) * 0.1
+    whd, bhd = wh.to(dev), bh.to(dev)
+    nslab = (C2 + 15) // 16
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    s = _lib.stream_ptr()
+
+    def run(mode, skip_f32, base=None, n_mean=0, img=None):
+        B_, X_ = (B, Xd) if img is None else (1, Xd[img * H * W:(img + 1) * H * W])
+        return run_b(B_, X_, mode, skip_f32, base, n_mean)
+
+    def run_b(B, Xd, mode, skip_f32, base, n_mean):
+        P = B * H * W
+        xs = torch.full((nslab * 2 * P * 16,), F16_NAN, dtype=torch.int16, device=dev)
+        ws, wsb, ctr = dx3_workspace(B, H, W, C1, N, dev)
+        acc = torch.empty(P * 16, device=dev)
+        feat = Xd.clone()
+        if skip_f32:
+            feat[:, C0:] = float("nan")  # never written when the fp32 stores are skipped
+        check(lib().idf_dx3_split_cols(s, P, 0, C0, ptr(feat), ld, ptr(xs), nslab, ptr(flag),
+                                       ptr(ws) if ws is not None else None,
+                                       ctr // 4 if ws is not None else 0), "split")
+        check(lib().idf_dx3_head_init(s, P, C0, ptr(feat), ld, ptr(whd), ldwh, ptr(bhd), nh,
+                                      ptr(acc)), "head init")
+        out = torch.zeros(P, 16, device=dev)
+        mean = torch.zeros(B * (nh // 2) * H * W, device=dev)
+        logs, scale = torch.zeros_like(mean), torch.zeros_like(mean)
+        for i, c in enumerate((C0, C1)):
+            hd = IdfDx3Head()
+            hd.w, hd.ldw, hd.n_head, hd.acc = ptr(whd), ldwh, nh, ptr(acc)
+            hd.last, hd.skip_f32 = int(i == 1), int(skip_f32)
+            hd.out.mode = mode
+            hd.out.out, hd.out.ld_out = ptr(out), 16
+            if base is not None:
+                hd.out.base, hd.out.ld_base = ptr(base), 16
+            hd.out.n_mean = n_mean
+            hd.out.mean, hd.out.logscale, hd.out.scale = ptr(mean), ptr(logs), ptr(scale)
+            check(lib().idf_conv3x3_dx3(s, B, H, W, c, ptr(xs), nslab, ptr(wdev[i]),
+                                        nf * ngroup, packs[i][1], ptr(b3), None, n_alloc, None, N,
+                                        ptr(feat) + 4 * c, ld, _lib.ACT["ReLU"], 0.01, ptr(flag),
+                                        ptr(ws), wsb, ctypes.byref(hd)), "dx3")
+        torch.cuda.synchronize()
+        return out.cpu(), feat.cpu(), (mean.cpu(), logs.cpu(), scale.cpu())
+
+    out, feat, _ = run(_lib.EPI_STORE, False)
+    ref = feat[:, :C2].double() @ wh[:, :C2].double().T + bh.double()
+    e = scaled_err(out[:, :nh], ref)
+    print(f"fused head {e:.2e}")
+    assert e <= 1e-5, e
+    assert not out[:, nh:].any()
+    hw = H * W
+    for i in sorted({0, B // 2, B - 1}):
+        alone = run(_lib.EPI_STORE, True, img=i)[0]
+        assert torch.equal(alone, out[i * hw:(i + 1) * hw]), ("batch", i)
+    out2, feat2, _ = run(_lib.EPI_STORE, True)
+    assert torch.equal(out2, out), "skipping the fp32 stores changed the head"
+    assert torch.isnan(feat2[:, C0:C2]).all(), "fp32 outputs written with skip_f32"
+    base = torch.round(torch.randn(P, 16, generator=g) * 256) / 256
+    r8 = torch.round(out[:, :nh] * 256) / 256
+    for mode, sign in ((_lib.EPI_COUPLE_ADD, 1), (_lib.EPI_COUPLE_SUB, -1)):
+        o3, _, _ = run(mode, True, base=base.to(dev))
+        assert torch.equal(o3[:, :nh], base[:, :nh] + sign * r8), mode
+    if nh % 2 == 0:
+        _, _, (mean, logs, scale) = run(_lib.EPI_PRIOR, True, n_mean=nh // 2)
+        h = out[:, :nh].view(B, H, W, nh).permute(0, 3, 1, 2)
+        assert torch.equal(mean.view(B, nh // 2, H, W), h[:, :nh // 2])
+        assert torch.equal(logs.view(B, nh // 2, H, W), h[:, nh // 2:])
+        assert torch.allclose(scale, torch.exp(logs), rtol=1e-6, atol=0)

@@ -200,3 +200,55 @@ def test_encode_fallback_beside_decode_exact(monkeypatch):
         assert bool((info_a["final_states"] == 1 << 32).all())
         assert bs_b.meta["conv"] == "f32"
         assert torch.equal(bs_b.states, ref_b.states) and torch.equal(bs_b.words, ref_b.words)
+
+
+@pytest.mark.parametrize("name,lvl,which", [("resflow-patches-vqvae", 0, "coupling"),
+                                            ("resflow-patches-vqvae", 0, "prior"),
+                                            ("resflows_smallpatch_split", 0, "coupling"),
+                                            ("resflows_smallpatch_split", 1, "coupling")])
+def test_fused_blocks_two_streams(name, lvl, which):
+    """A dense block with the fused head (dx3 layers + idf_dx3_head_init) run on two HIP streams
+    at once, each on its own workspace, gives the bits it gives alone: what two decode lanes
+    do.  (A head init staging its weights in LDS diverged here in 5-20 of 40 runs.)"""
+    from idfcodec import _lib, configs, synthetic
+    from idfcodec._lib import IdfHeadOut, ptr
+    eng = synthetic.build_model(configs.get(name)).cuda().engine()
+    Lv = eng.levels[lvl]
+    blk = eng.couple[lvl][0] if which == "coupling" else eng.prior[lvl]
+    assert blk.desc.fuse_head == 1 and blk.desc.dx3 == 1
+    B = 64
+    P = B * Lv.h * Lv.w
+    k0 = blk.geom.k_in[0]
+    g = torch.Generator().manual_seed(5)
+
+    def setup(slot):
+        ws = eng.workspace(B, slot)
+        x = (torch.randint(-64, 64, (P, k0), generator=g).float() / 256).cuda()
+        if which == "coupling":
+            x[:, Lv.a:] = 0.0  # the pad columns past a_ch
+        return ws, x, torch.zeros(P, 16, device="cuda")
+
+    def run(ws, x, out):
+        ws["feat"].view(-1, eng.ld_feat)[:P, :k0] = x
+        h = IdfHeadOut()
+        h.mode, h.out, h.ld_out = _lib.EPI_STORE, ptr(out), 16
+        blk.run(_lib.stream_ptr(), B, Lv.h, Lv.w, ptr(ws["feat"]), eng.ld_feat, ptr(ws["tmp"]),
+                eng.tmp_pitch(ws, P), h)
+
+    sets = [setup(1), setup(2)]
+    refs = []
+    for ws, x, out in sets:
+        run(ws, x, out)
+        torch.cuda.synchronize()
+        refs.append(out.clone())
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for rep in range(20):
+        for _, _, out in sets:
+            out.zero_()
+        torch.cuda.synchronize()
+        for st, (ws, x, out) in zip(streams, sets):
+            with torch.cuda.stream(st):
+                run(ws, x, out)
+        torch.cuda.synchronize()
+        for i, (_, _, out) in enumerate(sets):
+            assert torch.equal(out, refs[i]), (rep, i, int((out != refs[i]).any(1).sum()))

@@ -102,7 +102,7 @@ def main():
                 check(lib().idf_conv3x3_dx3(s, B, hw, hw, c_pad, ptr(xs), nsx, ptr(WD), g_alloc // 16,
                                             dsc, ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
                                             ptr(feat) + c_pad * 4, ld, 0, 0.0, ptr(flag), ptr(dws),
-                                            dwn), "dx3")
+                                            dwn, None), "dx3")
 
             # KB_ONLY=dx3r4: round 4's dx3 kernel (tools/ab_lib/dx3_r4/libdx3old.so, built from
             # that commit's conv3_dx3.hip) on the same box, same data -- its old ABI
