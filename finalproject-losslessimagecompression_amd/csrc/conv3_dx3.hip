@@ -59,10 +59,13 @@ typedef float d4 __attribute__((ext_vector_type(4)));
 typedef _Float16 e4 __attribute__((ext_vector_type(4)));
 typedef _Float16 e8 __attribute__((ext_vector_type(8)));
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef __bf16 b8 __attribute__((ext_vector_type(8)));
 
 struct Dx3Args {
-  const uint16_t* xs;  // split features [nslab_xs][2: hi, lo][P][16] f16 bits
+  const uint16_t* xs;  // split features [nslab_xs][2: hi, lo][P][16] f16 bits (bf16 kernel:
+                       // the block's bf16 shadow [P][16 nslab_xs], pixel-major)
   int64_t P;           // pixels of the batch (B * H * W)
+  int64_t xs_pix, xs_slab, xs_bytes;  // bytes: pixel to pixel, slab to slab, the whole buffer
   int32_t nslab_xs;    // slabs the split buffer holds
   int32_t C;           // input channels (slabs read: ceil(C / 16))
   const uint16_t* Wt;  // [nslab][ngroup][2: hi, lo][9 taps][NF][16 out][16 ch] f16 of w * 2^k
@@ -198,23 +201,25 @@ constexpr float kDxOutGuard = 8192.0f;
 // 10 x 20 (2 x 2 images of 8 x 8); 6 / 19: 4-wide images, four segments of 6 x 24; 26 / 17:
 // widths with one image edge inside a tile (two segments side by side, the second 8 slots past
 // the first's last lane: colbase = j mod 8).
-template <int NF, int WR, int PITCH, int PLANE_KIB>
+template <int NF, int WR, int PITCH, int PLANE_KIB, bool BF>
 struct Dx3Lds {
   static constexpr int T = WR * kDxWaves / 16;     // tiles per block
   static constexpr int HR = WR + 2;                // canvas rows a wave reads
-  static constexpr int NS = 5 * HR - 1;            // steps per slab (see the schedule)
+  static constexpr int NS = BF ? 2 * HR - 1 : 5 * HR - 1;  // steps per slab (the schedule)
+  static constexpr int NPL = BF ? 1 : 2;           // planes per tile canvas: xh, xl / x
   static constexpr int PLANE = PLANE_KIB * 1024;   // one plane (xh or xl) of a tile's canvas
   static constexpr int SLOTS = PLANE / 32;
-  static constexpr int WOFF = T * 2 * PLANE;       // weights within a stage
+  static constexpr int WOFF = T * NPL * PLANE;     // weights within a stage
   static constexpr int WPART = 9 * NF * 512;       // one part (wh or wl) of a slab's weights
-  static constexpr int WST = 2 * WPART;            // a multiple of 1 KiB: whole DMA pieces
+  // whole 1-KiB DMA pieces (the bf16 weights padded to them in HBM: packing.dxb_weights)
+  static constexpr int WST = BF ? (WPART + 1023) / 1024 * 1024 : 2 * WPART;
   static constexpr int STAGE = WOFF + WST;
   static constexpr int ZOFF = 2 * STAGE;           // NF * 512 B of zeros (the odd tap's pair)
   static constexpr int BOFF = ZOFF + NF * 512;     // bias table [16 classes][NF * 16] f32
   static constexpr int HOFF = BOFF + 16 * NF * 16 * 4;  // fused head weights [16][NF * 16] f32
   static constexpr int FOFF = HOFF + 16 * NF * 16 * 4;  // the split-K "last block" flag
   static constexpr int BYTES = FOFF + 16;
-  static constexpr int HPIECES = T * 2 * PLANE_KIB;        // halo DMA pieces per slab
+  static constexpr int HPIECES = T * NPL * PLANE_KIB;      // halo DMA pieces per slab
   static constexpr int WPIECES = WST / 1024;               // weight pieces per slab
   // piece slots per wave: halo slots [0, PH) then weight slots [PH, PPW); slot i of wave w is
   // piece w + 8 i of its kind (some slots of the last row of each kind are empty)
@@ -255,13 +260,15 @@ __device__ __forceinline__ DxTile dx_tile(const Dx3Args& g, int tile) {
   return t;
 }
 
-template <int NF, int WR, int PITCH, int PLANE_KIB>
+template <int NF, int WR, int PITCH, int PLANE_KIB, bool BF>
 __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
-  using L = Dx3Lds<NF, WR, PITCH, PLANE_KIB>;
+  using L = Dx3Lds<NF, WR, PITCH, PLANE_KIB, BF>;
   constexpr int T = L::T, HR = L::HR, NS = L::NS;
   static_assert(L::WST % 1024 == 0, "weight stage must be whole 1-KiB DMA pieces");
   static_assert(L::BYTES <= 160 * 1024, "LDS");
   static_assert(HR >= 3, "the A-fragment reads of a phase take its last three steps");
+  static_assert(IDF_DX3_DMAS == 0 || IDF_DX3_DMA0 + IDF_DX3_STAG + (L::PPW - 1) * IDF_DX3_DMAS < NS,
+                "every DMA piece of a slab is issued within the slab's steps");
   __shared__ __attribute__((aligned(16))) char lds[L::BYTES];
   int* last_flag = (int*)(lds + L::FOFF);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -285,8 +292,8 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   // (2 PLANE_KIB), plane (k / PLANE_KIB) % 2, canvas slots 32 (k % PLANE_KIB) .. +31 (lane:
   // slot + lane / 2, 8 channels (lane & 1)); weight pieces: 1 KiB of the slab's group weights.
   const int64_t plane_b = g.P * 32;                      // bytes of one plane of one slab
-  const uint32_t xs_stride = (uint32_t)(2 * plane_b);    // bytes per slab
-  const int64_t xs_bytes = (int64_t)g.nslab_xs * 2 * plane_b;
+  const uint32_t xs_stride = (uint32_t)g.xs_slab;        // bytes per slab
+  const int64_t xs_bytes = g.xs_bytes;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)g.xs, 0, (int)(xs_bytes < (int64_t)kDxInvalid ? xs_bytes : (int64_t)kDxInvalid), 0x00020000);
   const uint32_t wslab = (uint32_t)(g.ngroup * L::WST);  // weight bytes per slab
@@ -309,8 +316,8 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
     pbase[i] = kDxOff;
     plo[i] = 0;
     if (hk && pok[i]) {
-      const int t = k / (2 * PLANE_KIB), pl = (k / PLANE_KIB) % 2, pi = k % PLANE_KIB;
-      plo[i] = (t * 2 + pl) * L::PLANE + pi * 1024;
+      const int t = k / (L::NPL * PLANE_KIB), pl = (k / PLANE_KIB) % L::NPL, pi = k % PLANE_KIB;
+      plo[i] = (t * L::NPL + pl) * L::PLANE + pi * 1024;
       const int slot = 32 * pi + (lane >> 1);
       const int tt = tb * T + t;
       if (tt < g.ntiles) {
@@ -340,7 +347,7 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
         const int b = (dt.band * g.nby + iy) * g.nbx + ix;
         ok = ok && x >= 0 && x < g.Wd && ix < g.nbx && y >= 0 && y < g.H && iy < g.nby && b < g.B;
         if (ok)
-          pbase[i] = (uint32_t)(pl * plane_b + ((((int64_t)b * g.H + y) * g.Wd + x) * 32) + (lane & 1) * 16);
+          pbase[i] = (uint32_t)(pl * plane_b + ((((int64_t)b * g.H + y) * g.Wd + x) * g.xs_pix) + (lane & 1) * 16);
       }
     } else if (!hk && pok[i]) {
       plo[i] = L::WOFF + k * 1024;
@@ -405,7 +412,7 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   // ---- fragment read offsets (bytes from a stage base).  B (pixels): lane (q = lane >> 4,
   // j = lane & 15) reads pixel j of a canvas row, 8 channels.  A (weights): output j, 8 channels.
   const int slot0 = rowb * PITCH + colb;
-  const int tb0 = tw * 2 * L::PLANE;  // the wave's tile planes
+  const int tb0 = tw * L::NPL * L::PLANE;  // the wave's tile planes
   // [xh | xl] at (canvas row r0 + h, column j + dx): q 0,1 hi plane chunk q, q 2,3 lo plane chunk q-2
   const int oP = tb0 + (q >> 1) * L::PLANE + slot0 * 32 + (q & 1) * 16;
   // [xh(h, dx 0) | xh(h, dx 1)]
@@ -415,11 +422,12 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   // [wh(tap) ; wh(tap)] at tap t, fragment n: + (t * NF + n) * 512
   const int oAH = L::WOFF + j * 32 + (q & 1) * 16;
   // [wl(dy, 0) ; wl(dy, 1)]: + (3 dy * NF + n) * 512
-  const int oAF = L::WOFF + L::WPART + j * 32 + (q & 1) * 16 + (q >> 1) * NF * 512;
+  constexpr int WLO = BF ? 0 : L::WPART;  // the wl part (bf16 kernel: the only part)
+  const int oAF = L::WOFF + WLO + j * 32 + (q & 1) * 16 + (q >> 1) * NF * 512;
   // [wl(0, 2) ; wl(1, 2)]: + n * 512
-  const int oAG = L::WOFF + L::WPART + 2 * NF * 512 + j * 32 + (q & 1) * 16 + (q >> 1) * 3 * NF * 512;
+  const int oAG = L::WOFF + WLO + 2 * NF * 512 + j * 32 + (q & 1) * 16 + (q >> 1) * 3 * NF * 512;
   // [0 ; wl(2, 2)]: + n * 512; lanes q < 2 read the zero block (outside the stages)
-  const int oAO = L::WOFF + L::WPART + 8 * NF * 512 + j * 32 + (q & 1) * 16;
+  const int oAO = L::WOFF + WLO + 8 * NF * 512 + j * 32 + (q & 1) * 16;
   const bool zlane = q < 2;
   const char* zO = lds + L::ZOFF + j * 32 + (q & 1) * 16;
 
@@ -432,6 +440,9 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   auto rd = [](const char* p) { return *(const e8*)p; };
   auto mma = [](const e8& a, const e8& bb, d4& c) {
     if (IDF_DX3_ABLATE & 16) c[0] += (float)(a[0] * bb[0]);
+    else if constexpr (BF)
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8, a), __builtin_bit_cast(b8, bb),
+                                                   c, 0, 0, 0);
     else c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bb, c, 0, 0, 0);
   };
   auto rdB = [&](const char* p) -> e8 {
@@ -488,17 +499,11 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
     DX3_STAMP(s - s0, 1);
     if (s == s0) DX3_TL(2);
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int dy = 0; dy < 3; ++dy) read_A(cur, 0, dy, AS[0][dy]);
-#pragma unroll
-    for (int k = 0; k < DB; ++k) Bq[k] = read_B(cur, k);
     const bool more = s + 1 < s1;
     const int nst = (s + 1 - s0) & 1;
-    auto step = [&](auto tc) {
+    // slab s + 1's DMA at step t: one piece every IDF_DX3_DMAS steps from step IDF_DX3_DMA0
+    auto dma_step = [&](auto tc) {
       constexpr int t = decltype(tc)::value;
-      if (IDF_DX3_SB) __builtin_amdgcn_sched_barrier(0);  // keep the schedule: steps do not mix
-      if constexpr (t == 9) DX3_STAMP(s - s0, 2);
-      // slab s + 1's DMA, one piece every IDF_DX3_DMAS steps from step IDF_DX3_DMA0
       constexpr int ds = IDF_DX3_DMAS > 0 ? IDF_DX3_DMAS : 1;
       auto dma_at = [&](auto dtc) {
         constexpr int dt_ = decltype(dtc)::value;
@@ -513,6 +518,62 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
       };
       if (IDF_DX3_STAG == 0 || !(wave & 4)) dma_at(std::integral_constant<int, t - IDF_DX3_DMA0>{});
       else dma_at(std::integral_constant<int, t - IDF_DX3_DMA0 - IDF_DX3_STAG>{});
+    };
+    if constexpr (BF) {
+      // bf16: one product per tap, the F / G phases of the split schedule on the one plane:
+      //   steps [0, HR)       (F, h = t):      [w(dy,0) ; w(dy,1)] . [x(h,0) | x(h,1)]
+      //   steps [HR, 2HR - 1) (G, h = t - HR): [w(0,2) ; w(1,2)] and [0 ; w(2,2)]
+      //                                        . [x(h,2) | x(h+1,2)]
+      // 5 MFMAs per 16 channels and row (4.5 the floor); the F weights read at the slab's
+      // start, the G pairs in its steps 1 and 2
+      auto read_Bf = [&](const char* st, int t) -> e8 {
+        if (t < HR) return rdB(st + oF + t * PITCH * 32);
+        return rdB(st + oG + (t - HR) * PITCH * 32);
+      };
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) read_A(cur, 3, dy, AS[1][dy]);
+#pragma unroll
+      for (int k = 0; k < DB; ++k) Bq[k] = read_Bf(cur, k);
+      auto stepb = [&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        if (IDF_DX3_SB) __builtin_amdgcn_sched_barrier(0);
+        dma_step(tc);
+        if constexpr (t == 1 || t == 2) {
+#pragma unroll
+          for (int n = 0; n < NF; ++n) {
+            if (t == 1) AZ[0][n] = rdA(cur + oAG + n * 512);
+            else AZ[1][n] = rdA(zlane ? zO + n * 512 : cur + oAO + n * 512);
+          }
+        }
+        if constexpr (t + DB < NS) Bq[(t + DB) % RB] = read_Bf(cur, t + DB);
+        const e8& Bv = Bq[t % RB];
+        if constexpr (t < HR) {
+          mma_rows(AS[1], Bv, t);
+        } else {
+          constexpr int h = t - HR;
+          if constexpr (h < WR) {
+#pragma unroll
+            for (int n = 0; n < NF; ++n) mma(AZ[0][n], Bv, acc[h][n]);
+          }
+          if constexpr (h > 0) {
+#pragma unroll
+            for (int n = 0; n < NF; ++n) mma(AZ[1][n], Bv, acc[h - 1][n]);
+          }
+        }
+      };
+      dx_unroll(stepb, std::make_integer_sequence<int, NS>{});
+      DX3_STAMP(s - s0, 3);
+      continue;
+    }
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) read_A(cur, 0, dy, AS[0][dy]);
+#pragma unroll
+    for (int k = 0; k < DB; ++k) Bq[k] = read_B(cur, k);
+    auto step = [&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      if (IDF_DX3_SB) __builtin_amdgcn_sched_barrier(0);  // keep the schedule: steps do not mix
+      if constexpr (t == 9) DX3_STAMP(s - s0, 2);
+      dma_step(tc);
       // weights of the next phase, one kernel row per step, in the first three steps of the
       // phase before it (its register set was freed by the phase before that)
       if constexpr (t < 3) read_A(cur, 1, t, AS[1][t]);
@@ -659,7 +720,7 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
         for (int k = 0; k < 4; ++k) {
           const float t = acc[m][n][k] * g.yscale + bv[k];
           v[k] = act.tanh_ ? wact(t, g.act, g.slope) : act(t);
-          if (row_ok) out_ok = out_ok && fabsf(v[k]) < kDxOutGuard;
+          if (!BF && row_ok) out_ok = out_ok && fabsf(v[k]) < kDxOutGuard;
         }
         if (row_ok && !g.skip_f32) {
           if (n0 + 4 <= g.N) {
@@ -683,11 +744,16 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
       }
       const int c = g.C + n0;  // split channel of v[0]; c % 4 == 0, so v stays in one slab
       if (row_ok && !(IDF_DX3_ABLATE & 128) && c < zend) {
-        const e4 h = __builtin_convertvector(v, e4);
-        const e4 l = __builtin_convertvector(v - __builtin_convertvector(h, d4), e4);
-        char* p = xsb + (int64_t)(c >> 4) * 2 * plane_b + pix * 32 + (c & 15) * 2;
-        *(e4*)p = h;
-        *(e4*)(p + plane_b) = l;
+        if constexpr (BF) {  // the bf16 shadow, round to nearest even
+          typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+          *(b4*)(xsb + pix * g.xs_pix + c * 2) = __builtin_convertvector(v, b4);
+        } else {
+          const e4 h = __builtin_convertvector(v, e4);
+          const e4 l = __builtin_convertvector(v - __builtin_convertvector(h, d4), e4);
+          char* p = xsb + (int64_t)(c >> 4) * 2 * plane_b + pix * 32 + (c & 15) * 2;
+          *(e4*)p = h;
+          *(e4*)(p + plane_b) = l;
+        }
       }
     }
     if (fh) {
@@ -984,16 +1050,28 @@ extern "C" int idf_dx3_head_init(void* stream, int64_t P, int32_t C0, const floa
   return idf_last_error();
 }
 
-extern "C" int idf_conv3x3_dx3(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
-                               uint16_t* xs, int32_t nslab_xs, const uint16_t* w, int32_t nft,
-                               float yscale, const float* b3, const float* vtap, int32_t ldv,
-                               const float* bfull, int32_t N, float* out, int64_t ld_out,
-                               int32_t act, float slope, uint32_t* d_flag, void* d_workspace,
-                               int64_t workspace_bytes, const IdfDx3Head* head) {
+// the bf16 kernel's geometries: the 16-wide canvas (tiles and gutter packing) and the 8 x 8
+// level's segments, one output group of up to 3 fragments (the bf16 blocks' growth <= 48)
+static bool dxb_plan_ok(const Dx3Plan& p) {
+  return p.ok && p.nf <= 3 && p.ngroup == 1 && (p.pitch == 18 || p.pitch == 10);
+}
+
+extern "C" int idf_conv3x3_dxb_supported(int32_t H, int32_t W, int32_t N) {
+  return dxb_plan_ok(dx3_plan(H, W, N)) ? 1 : 0;
+}
+
+// One dx3 launch, split-f16 (bf = false: xs the split copy) or bf16 (bf = true: xs the bf16
+// shadow).  xs_pix / xs_slab / xs_bytes: the buffer's pixel and slab strides and size, bytes.
+static int dx3_run(void* stream, bool bf, int32_t B, int32_t H, int32_t W, int32_t C, uint16_t* xs,
+                   int64_t xs_pix, int64_t xs_slab, int64_t xs_bytes, int32_t nslab_xs,
+                   const uint16_t* w, int32_t nft, float yscale, const float* b3,
+                   const float* vtap, int32_t ldv, const float* bfull, int32_t N, float* out,
+                   int64_t ld_out, int32_t act, float slope, uint32_t* d_flag, void* d_workspace,
+                   int64_t workspace_bytes, const IdfDx3Head* head) {
   if (B <= 0 || H <= 0 || W <= 0 || N <= 0) return IDF_OK;
   if (C <= 0 || (C & 3) || !w || !xs || !out || !b3) return IDF_ERR_ARG;
   const Dx3Launch sh = dx3_launch_shape(B, H, W, C, N);
-  if (!sh.pl.ok) return IDF_ERR_UNSUPPORTED;
+  if (!sh.pl.ok || (bf && !dxb_plan_ok(sh.pl))) return IDF_ERR_UNSUPPORTED;
   // the weights hold exactly the kernel's fragments: ngroup groups of nf, nft = ngroup * nf
   if (nft != sh.pl.ngroup * sh.pl.nf) return IDF_ERR_ARG;
   if (vtap && (!bfull || ldv < N)) return IDF_ERR_ARG;
@@ -1002,7 +1080,7 @@ extern "C" int idf_conv3x3_dx3(void* stream, int32_t B, int32_t H, int32_t W, in
   const int64_t P = (int64_t)B * H * W;
   // 32-bit buffer offsets, and kDxOff past the end of every slab: the split buffer must span
   // < 2 GiB (imagenet64's 32x32 level: B < ~960 images)
-  if (idf_dx3_split_bytes(P, 16 * nslab_xs) >= (int64_t)kDxOff) return IDF_ERR_UNSUPPORTED;
+  if (xs_bytes >= (int64_t)kDxOff) return IDF_ERR_UNSUPPORTED;
   const int64_t nblk = (int64_t)sh.nblk_tiles * sh.pl.ngroup * sh.nchunk;
   if (sh.ntiles >= (1 << 20) || nblk >= (1 << 20)) return IDF_ERR_UNSUPPORTED;  // udiv_s operands
   Dx3Args g = {};
@@ -1014,6 +1092,7 @@ extern "C" int idf_conv3x3_dx3(void* stream, int32_t B, int32_t H, int32_t W, in
     g.part = (float*)((char*)d_workspace + cb);
   }
   g.xs = xs; g.P = P; g.nslab_xs = nslab_xs; g.C = C;
+  g.xs_pix = xs_pix; g.xs_slab = xs_slab; g.xs_bytes = xs_bytes;
   g.Wt = w; g.nslab = sh.nslab; g.ngroup = sh.pl.ngroup; g.N = N;
   g.B = B; g.H = H; g.Wd = W;
   g.nbx = sh.pl.nbx; g.nby = sh.pl.nby;
@@ -1049,7 +1128,9 @@ extern "C" int idf_conv3x3_dx3(void* stream, int32_t B, int32_t H, int32_t W, in
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)nblk), blk(kDxThreads);
 #define IDF_DX3_GO(nf_, wr_, pitch_, kib_) \
-  hipLaunchKernelGGL((conv3_dx3_kernel<nf_, wr_, pitch_, kib_>), grid, blk, 0, s, g)
+  hipLaunchKernelGGL((conv3_dx3_kernel<nf_, wr_, pitch_, kib_, false>), grid, blk, 0, s, g)
+#define IDF_DXB_GO(nf_, wr_, pitch_, kib_) \
+  hipLaunchKernelGGL((conv3_dx3_kernel<nf_, wr_, pitch_, kib_, true>), grid, blk, 0, s, g)
 #define IDF_DX3_NF(wr_, pitch_, kib_)                      \
   switch (sh.pl.nf) {                                      \
     case 1: IDF_DX3_GO(1, wr_, pitch_, kib_); break;       \
@@ -1058,7 +1139,22 @@ extern "C" int idf_conv3x3_dx3(void* stream, int32_t B, int32_t H, int32_t W, in
     default: IDF_DX3_GO(4, wr_, pitch_, kib_); break;      \
   }
   constexpr int W2 = 16 / kDxWaves, W4 = 32 / kDxWaves;  // rows per wave: one tile / two tiles
-  if (sh.T == 2) {
+  if (bf) {
+#define IDF_DXB_NF(wr_, pitch_, kib_)                 \
+  switch (sh.pl.nf) {                                 \
+    case 1: IDF_DXB_GO(1, wr_, pitch_, kib_); break;  \
+    case 2: IDF_DXB_GO(2, wr_, pitch_, kib_); break;  \
+    default: IDF_DXB_GO(3, wr_, pitch_, kib_); break; \
+  }
+    if (sh.T == 2) {
+      IDF_DXB_NF(W4, 18, 11)
+    } else if (sh.pl.pitch == 18) {
+      IDF_DXB_NF(W2, 18, 11)
+    } else {
+      IDF_DXB_NF(W2, 10, 13)
+    }
+#undef IDF_DXB_NF
+  } else if (sh.T == 2) {
     switch (sh.pl.nf) {
       case 1: IDF_DX3_GO(1, W4, 18, 11); break;
       case 2: IDF_DX3_GO(2, W4, 18, 11); break;
@@ -1073,5 +1169,32 @@ extern "C" int idf_conv3x3_dx3(void* stream, int32_t B, int32_t H, int32_t W, in
   }
 #undef IDF_DX3_NF
 #undef IDF_DX3_GO
+#undef IDF_DXB_GO
   return idf_last_error();
+}
+
+extern "C" int idf_conv3x3_dx3(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
+                               uint16_t* xs, int32_t nslab_xs, const uint16_t* w, int32_t nft,
+                               float yscale, const float* b3, const float* vtap, int32_t ldv,
+                               const float* bfull, int32_t N, float* out, int64_t ld_out,
+                               int32_t act, float slope, uint32_t* d_flag, void* d_workspace,
+                               int64_t workspace_bytes, const IdfDx3Head* head) {
+  const int64_t P = (int64_t)B * H * W;
+  return dx3_run(stream, false, B, H, W, C, xs, 32, 2 * P * 32, idf_dx3_split_bytes(P, 16 * nslab_xs),
+                 nslab_xs, w, nft, yscale, b3, vtap, ldv, bfull, N, out, ld_out, act, slope, d_flag,
+                 d_workspace, workspace_bytes, head);
+}
+
+extern "C" int idf_conv3x3_dxb(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
+                               uint16_t* x16, int64_t ld_x16, const uint16_t* w, int32_t nft,
+                               const float* b3, const float* vtap, int32_t ldv, const float* bfull,
+                               int32_t N, float* out, int64_t ld_out, int32_t act, float slope,
+                               void* d_workspace, int64_t workspace_bytes,
+                               const IdfDx3Head* head) {
+  // the shadow's rows are whole 16-channel slabs, 16-B aligned; its outputs' slab must exist
+  if ((ld_x16 & 15) || (uintptr_t)x16 % 16 || (C + N + 15) / 16 * 16 > ld_x16) return IDF_ERR_ARG;
+  const int64_t P = (int64_t)B * H * W;
+  return dx3_run(stream, true, B, H, W, C, x16, 2 * ld_x16, 32, P * ld_x16 * 2, (int32_t)(ld_x16 / 16),
+                 w, nft, 1.0f, b3, vtap, ldv, bfull, N, out, ld_out, act, slope, nullptr,
+                 d_workspace, workspace_bytes, head);
 }

@@ -609,20 +609,35 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
   int64_t ld16 = 0;
   float* ws = tmp;
   int64_t ws_floats = P * ld_tmp;
+  // bf16 blocks on the bf16 direct conv (IdfDenseBlock.dxb, conv3_dx3.hip): every layer, by
+  // the level geometry alone; the split-K workspace after the shadow, its counters zeroed here
+  bool dxb = false;
   if (blk->bf16) {
     if (!blk->fold) return IDF_ERR_ARG;
-    for (int i = 0; i < blk->depth; ++i)
+    dxb = blk->dxb && blk->depth > 0 && idf_conv3x3_dxb_supported(H, W, blk->g_pad);
+    for (int i = 0; i < blk->depth; ++i) {
       if (!blk->wb16[i]) return IDF_ERR_ARG;
+      if (dxb && !blk->dxb_w[i]) return IDF_ERR_ARG;
+    }
     // pitch a multiple of 64 channels: a pixel's 32-channel slab is one aligned 64-B run
     ld16 = ((int64_t)blk->k_in[blk->depth] + 63) / 64 * 64;
-    const int64_t sh = (P * ld16 / 2 + 3) / 4 * 4;  // floats
-    if (sh > ws_floats) return IDF_ERR_WORKSPACE;
+    const int64_t sh = dxb ? (P * ld16 / 2 + 63) / 64 * 64 : (P * ld16 / 2 + 3) / 4 * 4;  // floats
+    if (sh > ws_floats || (dxb && (uintptr_t)tmp % 256)) return IDF_ERR_WORKSPACE;
     f16 = (uint16_t*)tmp;
     ws = tmp + sh;
     ws_floats -= sh;
     const int c0 = blk->k_in[0];
-    int rc = idf_f32_to_bf16_cols(stream, P, c0, (c0 + 7) / 8 * 8, feat, ld_feat, f16, ld16);
+    // zeros on to the next 8 channels (conv3_bf16's k-blocks) / 16 (dxb's slabs)
+    int rc = idf_f32_to_bf16_cols(stream, P, c0, dxb ? (c0 + 15) / 16 * 16 : (c0 + 7) / 8 * 8,
+                                  feat, ld_feat, f16, ld16);
     if (rc) return rc;
+    if (dxb) {
+      const int64_t need = idf_conv3x3_dx3_workspace(B, H, W, blk->k_in[blk->depth - 1], blk->g_pad);
+      if (need < 0 || need > ws_floats * 4) return IDF_ERR_WORKSPACE;
+      if (need > 0 && hipMemsetAsync(ws, 0, (size_t)idf_conv3x3_dx3_counter_bytes(B, H, W, blk->g_pad),
+                                     s) != hipSuccess)
+        return IDF_ERR_HIP;
+    }
   }
   // dx3 blocks keep the split copy of their feature columns (conv3_dx3.hip) at the front of
   // tmp: the block input is split once here, every dx3 layer writes its outputs in both
@@ -690,7 +705,12 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
       const bool wino = blk->wino && blk->wino_u[i] && idf_conv3x3_wino_supported(H, W);
       const bool bf = blk->bf16 != 0;
       const int n16 = (c + blk->g_pad + 7) / 8 * 8 - c;
-      int rc = bf
+      int rc = (bf && dxb)
+                   ? idf_conv3x3_dxb(stream, B, H, W, c, f16, ld16, blk->dxb_w[i], dx3_nft,
+                                     blk->b3[i], blk->vtap[i], blk->ldv, blk->bfull[i], blk->g_pad,
+                                     feat + c, ld_feat, blk->act, blk->slope, ws, ws_floats * 4,
+                                     nullptr)
+               : bf
                    ? idf_conv3x3_bf16(stream, B, H, W, c, f16, ld16, blk->wb16[i], blk->g_alloc,
                                       blk->b3[i], blk->vtap[i], blk->ldv, blk->bfull[i],
                                       blk->g_pad, feat + c, ld_feat, f16 + c, ld16, n16,

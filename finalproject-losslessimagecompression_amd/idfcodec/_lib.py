@@ -57,6 +57,7 @@ class IdfDenseBlock(ctypes.Structure):
         ("wx3", i32), ("wx3_yscale", f32 * MAX_DEPTH), ("wx3_u", P * MAX_DEPTH), ("range_flag", P),
         ("dx3", i32), ("dx3_yscale", f32 * MAX_DEPTH), ("dx3_w", P * MAX_DEPTH),
         ("fuse_head", i32), ("keep_feat", i32),
+        ("dxb", i32), ("dxb_w", P * MAX_DEPTH),
     ]
 
 
@@ -127,6 +128,9 @@ SIGNATURES = {
     "idf_conv3x3_dx3_workspace": (i64, [i32, i32, i32, i32, i32]),
     "idf_dx3_split_bytes": (i64, [i64, i32]),
     "idf_dx3_split_cols": (ctypes.c_int, [P, i64, i32, i32, P, i64, P, i32, P, P, i32]),
+    "idf_conv3x3_dxb_supported": (ctypes.c_int, [i32, i32, i32]),
+    "idf_conv3x3_dxb": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, P, P, i32, P, i32,
+                                       P, i64, i32, f32, P, i64, P]),
     "idf_conv3x3_bf16_workspace": (i64, [i32, i32, i32, i32, i32]),
     "idf_conv3x3_bf16": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, P, P, i32, P, i32,
                                         P, i64, P, i64, i32, i32, f32, P, i64]),
@@ -188,7 +192,7 @@ def require_device(t: torch.Tensor, what: str = "tensor"):
         raise IdfError(f"idfcodec: {what} must be a HIP device tensor (no CPU fallback)")
 
 
-def new_stream(device=None) -> torch.cuda.ExternalStream:
+def new_stream(device=None, priority: int | None = None) -> torch.cuda.ExternalStream:
     """A HIP stream created with hipStreamNonBlocking on `device`, as a torch stream.
     The ImageCodec lanes use these: two torch.cuda.Stream()s were measured NOT to run
     concurrently on MI355X (the second lane's kernels waited ~25 ms for the first's), two
@@ -196,7 +200,11 @@ def new_stream(device=None) -> torch.cuda.ExternalStream:
     hip = ctypes.CDLL("libamdhip64.so.7")
     h = ctypes.c_void_p()
     with torch.cuda.device(device):
-        rc = hip.hipStreamCreateWithFlags(ctypes.byref(h), ctypes.c_uint(1))
+        if priority is None:
+            rc = hip.hipStreamCreateWithFlags(ctypes.byref(h), ctypes.c_uint(1))
+        else:  # hipStreamCreateWithPriority: lower numbers run first
+            rc = hip.hipStreamCreateWithPriority(ctypes.byref(h), ctypes.c_uint(1),
+                                                 ctypes.c_int(int(priority)))
     if rc != 0:
         raise IdfError(f"hipStreamCreateWithFlags failed ({rc})")
     return torch.cuda.ExternalStream(h.value, device=device)

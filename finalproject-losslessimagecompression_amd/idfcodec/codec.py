@@ -32,11 +32,13 @@ FLAG_CONV_X3 = 1
 # that predates the field (halo / gemm / unfold / bf16): a version-1 file with flags 0 reads as
 # conv "unrecorded", which any engine but a split-f16 one may decode (the pre-field behaviour).
 # 6: round 4's dx3 (direct split-f16 only at widths a multiple of 16: engine mode 'dx3w16');
-# 7: dx3 on every geometry conv3_dx3.hip packs (imagenet64's 8x8 level too)
+# 7: dx3 on every geometry conv3_dx3.hip packs (imagenet64's 8x8 level too); 8: bf16 engines on
+# the bf16 direct conv (engine mode 'dxb'; 5 = conv3_bf16.hip)
 CONV_CODES = {"f32": 0, "x3": 1, "halo": 2, "gemm": 3, "unfold": 4, "bf16": 5, "dx3w16": 6,
-              "dx3": 7}
-# the split-f16 / exact-f32 modes one engine switches between per bitstream (engine.CONV_MODES)
-SWITCHABLE = ("dx3", "dx3w16", "x3", "f32")
+              "dx3": 7, "dxb": 8}
+# the modes one engine switches between per bitstream (engine.can_run says which it has):
+# split-f16 / exact-f32 for fp32 engines (engine.CONV_MODES), dxb / bf16 for bf16 engines
+SWITCHABLE = ("dx3", "dx3w16", "x3", "f32", "dxb", "bf16")
 SPLIT_F16 = ("dx3", "dx3w16", "x3")
 CONV_NAMES = {v: k for k, v in CONV_CODES.items()}
 
@@ -556,8 +558,11 @@ class ImageCodec:
         return [B // n] * n
 
     def _lane_streams(self, n: int):
+        # IDF_LANE_PRIO=1: lane 0's stream at the device's greatest priority (timing A/B)
+        prio = os.environ.get("IDF_LANE_PRIO", "0") == "1"
         while len(self._streams) < n:
-            self._streams.append(_lib.new_stream(self.engine.device))
+            p = -1 if (prio and not self._streams) else None
+            self._streams.append(_lib.new_stream(self.engine.device, priority=p))
         return self._streams[:n]
 
     def check_bitstream(self, bs: Bitstream):
@@ -591,8 +596,7 @@ class ImageCodec:
             return
         if conv not in CONV_CODES:
             raise ValueError(f"unknown conv mode {conv!r}")
-        switchable = conv in SWITCHABLE and have in SWITCHABLE and (
-            conv == "f32" or (conv == "x3" and eng.wx3) or (conv in ("dx3", "dx3w16") and eng.dx3))
+        switchable = conv in SWITCHABLE and have in SWITCHABLE and eng.can_run(conv)
         if conv != have and not switchable:
             raise ValueError(f"bitstream was coded with {conv!r} convs; this engine runs "
                              f"{have!r} (IDF_FOLD / IDF_WINO / IDF_HALO / precision differ): "

@@ -60,6 +60,12 @@ DX3 = os.environ.get("IDF_DX3", "1") != "0"
 # keeps the GEMM heads (timing A/B only: the head's sums run in another order, so encoder and
 # decoder must agree on it).
 HEAD_FUSE = os.environ.get("IDF_HEAD_FUSE", "1") != "0"
+# bf16 engines (configs naming bf16 coupling convs) run their DenseLayers as the bf16 direct
+# conv (conv mode "dxb", idf_conv3x3_dxb: the dx3 kernel's tiling and LDS-DMA with one bf16
+# product per tap) where the level geometry allows, conv3_bf16.hip ("bf16", round 4's) elsewhere
+# and when IDF_DXB=0.  The two sum in different orders: a bitstream records which ran.
+DXB = os.environ.get("IDF_DXB", "1") != "0"
+BF16_MODES = ("dxb", "bf16")
 
 
 class DeviceBlock:
@@ -81,6 +87,7 @@ class DeviceBlock:
         self.wb16 = [dev(a.view(np.int16)) for a in packed.wb16]
         self.wx3_u = [dev(a.view(np.int16)) for a in packed.wx3_u]
         self.dx3_w = [dev(a.view(np.int16)) for a in packed.dx3_w]
+        self.dxb_w = [dev(a.view(np.int16)) for a in packed.dxb_w]
         d = IdfDenseBlock()
         g = self.geom
         d.depth = g.depth
@@ -128,6 +135,9 @@ class DeviceBlock:
         d.bf16 = 1 if (packed.fold and self.wb16) else 0
         for i, u in enumerate(self.wb16):
             d.wb16[i] = u.data_ptr()
+        d.dxb = 1 if (d.bf16 and self.dxb_w and DXB) else 0
+        for i, u in enumerate(self.dxb_w):
+            d.dxb_w[i] = u.data_ptr()
         d.ldv = packed.g_alloc
         for i in range(len(self.vtap)):
             d.vtap[i] = self.vtap[i].data_ptr()
@@ -276,6 +286,9 @@ class FlowEngine:
         for b in blocks:
             b.desc.range_flag = self.range_flag.data_ptr()
         self.conv_mode = "dx3" if self.dx3 else ("x3" if self.wx3 else "f32")
+        self.dxb = self.precision == "bf16" and DXB and any(b.dxb_w for b in blocks)
+        if self.precision == "bf16":
+            self.conv_mode = "dxb" if self.dxb else "bf16"
         self.ld_feat = max(b.geom.ld_feat for b in blocks)
         # tmp: split-K partials (f32); bf16 blocks also keep their bf16 feature shadow at its
         # front (pitch round_up(k, 64) bf16 = half as many floats) ahead of 2-way partials
@@ -321,6 +334,14 @@ class FlowEngine:
         elsewhere), 'x3' (split-f16 Winograd everywhere; both need the split weights) or 'f32'
         (exact-f32 Winograd).  The decoder must run the mode the encoder ran
         (Bitstream.meta['conv'])."""
+        if self.precision == "bf16":
+            if mode not in BF16_MODES or (mode == "dxb" and not self.dxb):
+                raise ValueError(f"this bf16 engine runs conv modes "
+                                 f"{BF16_MODES if self.dxb else ('bf16',)}, not {mode!r}")
+            for b in self._blocks:
+                b.desc.dxb = 1 if (mode == "dxb" and b.dxb_w) else 0
+            self.conv_mode = mode
+            return
         if mode not in CONV_MODES:
             raise ValueError(f"conv mode must be one of {CONV_MODES}, not {mode!r}")
         if mode == "x3" and not self.wx3:
@@ -345,12 +366,21 @@ class FlowEngine:
         LDS-halo kernel), 'gemm' (folded implicit GEMM) or 'unfold' (the reference's 1x1 +
         3x3, IDF_FOLD=0)."""
         if self.precision == "bf16":
-            return "bf16"
+            return self.conv_mode  # "dxb" or "bf16"
         if not self.fold:
             return "unfold"
         if self.wino:
             return self.conv_mode
         return "halo" if HALO else "gemm"
+
+    def can_run(self, conv: str) -> bool:
+        """This engine can switch to conv mode `conv` (a bitstream's recorded arithmetic)."""
+        if self.precision == "bf16":
+            return conv == "bf16" or (conv == "dxb" and self.dxb)
+        if not (self.fold and self.wino):
+            return False
+        return conv == "f32" or (conv == "x3" and self.wx3) or (
+            conv in ("dx3", "dx3w16") and self.dx3)
 
     def clear_range_flag(self):
         self.range_flag.zero_()
@@ -420,7 +450,7 @@ class FlowEngine:
             P = B * Lv.h * Lv.w
             extra = 0
             for b in self.couple[l] + [self.prior[l]]:
-                nd = len(b.dx3_w)
+                nd = len(b.dx3_w) or len(b.dxb_w)  # dxb: every layer (the bf16 shadow's tail)
                 if nd:
                     w = lib().idf_conv3x3_dx3_workspace(B, Lv.h, Lv.w, b.geom.k_in[nd - 1],
                                                         b.geom.g_pad)

@@ -116,6 +116,7 @@ class PackedBlock:
     wx3_yscale: list = field(default_factory=list)
     dx3_w: list = field(default_factory=list)    # fold+dx3: dx3_weights() per layer (uint16)
     dx3_yscale: list = field(default_factory=list)
+    dxb_w: list = field(default_factory=list)    # fold+bf16: dxb_weights() per layer (uint16)
 
 
 def fold_layer(w1, b1, w3):
@@ -255,6 +256,33 @@ def bf16_weights(w: np.ndarray, C: int) -> np.ndarray:
     return np.ascontiguousarray(b)
 
 
+def dxb_weights(w: np.ndarray, C: int) -> np.ndarray:
+    """bf16 direct-conv weights for idf_conv3x3_dxb (conv3_dx3.hip, bf16 kernel).
+
+    w: [n_alloc <= 48][9][ldw] fp32 folded 3x3 weights (padded coordinates), C = the layer's
+    padded input channels.  Returns uint16 bf16 bits (round to nearest even, the values
+    bf16_weights holds) as [nslab = ceil(C/16)][9 taps][nf][16 out][16 ch] per slab, each slab
+    zero-padded to whole KiB (the kernel's 1-KiB DMA pieces): the A-operand fragments one kernel
+    block stages into LDS verbatim.  Channels at or past C are zero (the kernel reads the last
+    slab up to the next multiple of 16, where its own outputs land)."""
+    import torch
+    n_alloc = w.shape[0]
+    assert n_alloc % 16 == 0 and n_alloc <= 48
+    nf = n_alloc // 16
+    nslab = (C + 15) // 16
+    g = np.zeros((n_alloc, 9, nslab * 16), np.float32)
+    cw = min(w.shape[2], C)
+    g[:, :, :cw] = w[:, :, :cw]
+    b = torch.from_numpy(g).to(torch.bfloat16).view(torch.int16).numpy().view(np.uint16)
+    b = b.reshape(nf, 16, 9, nslab, 16).transpose(3, 2, 0, 1, 4)  # slab, tap, f, r, c
+    per = 9 * nf * 256                                             # elements of a slab
+    pad = (per * 2 + 1023) // 1024 * 1024 // 2
+    out = np.zeros((nslab, pad), np.uint16)
+    out[:, :per] = b.reshape(nslab, per)
+    assert C % 16 == 0 or not b[-1, ..., C % 16:].any(), "dxb weights past C not zero"
+    return np.ascontiguousarray(out)
+
+
 def interior_bias(b3: np.ndarray, v: np.ndarray) -> np.ndarray:
     """b3 + v[0] + ... + v[8], sequential fp32 adds: the order the device's border
     loop uses, so interior and border pixels see the same arithmetic."""
@@ -288,7 +316,7 @@ def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
     geom = BlockGeometry(a=a, depth=depth, growth=gs, n_head=n_head)
     g_alloc = round_up(geom.g_pad, tile_n(geom.g_pad))
     w1s, b1s, w3s, b3s, n1s, ld1s, ld3s = [], [], [], [], [], [], []
-    vts, bfs, wus, wbs, wxs, wys, wds, wdy = [], [], [], [], [], [], [], []
+    vts, bfs, wus, wbs, wxs, wys, wds, wdy, wdbs = [], [], [], [], [], [], [], [], []
     c = a
     for i in range(depth):
         k = geom.k_in[i]
@@ -333,6 +361,7 @@ def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
                         f"bf16 DenseLayer convs take growth <= 48 per layer (conv3_bf16.hip: "
                         f"one 48-output tile per block); this layer grows by {g}")
                 wbs.append(bf16_weights(w3p, k))
+                wdbs.append(dxb_weights(w3p, k))
             vp = np.zeros((9, g_alloc), np.float32)
             vp[:, :g] = v
             vts.append(vp)
@@ -351,7 +380,7 @@ def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
     bhp = np.zeros(nh_alloc, np.float32)
     bhp[:n_head] = arr(f"layers.{depth}.bias")
     return PackedBlock(geom, act, slope, fold, vts, bfs, w1s, b1s, w3s, b3s, whp, bhp, g_alloc,
-                       n1s, ld1s, ld3s, nh_alloc, ldwh, wus, wbs, wxs, wys, wds, wdy)
+                       n1s, ld1s, ld3s, nh_alloc, ldwh, wus, wbs, wxs, wys, wds, wdy, wdbs)
 
 
 def unpack_features(feat: np.ndarray, geom: BlockGeometry, n: int) -> np.ndarray:

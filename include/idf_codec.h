@@ -213,6 +213,11 @@ typedef struct IdfDenseBlock {
    * the GEMM's, so the flag is part of the conv arithmetic an encoder and its decoder share. */
   int32_t fuse_head;
   int32_t keep_feat;
+  /* dxb = 1 (with bf16 = 1): a block whose geometry idf_conv3x3_dxb_supported takes runs every
+   * layer as the bf16 direct conv (idf_conv3x3_dxb) with the weights dxb_w[i] (all set) instead
+   * of idf_conv3x3_bf16 -- another sum order, so it is part of the conv arithmetic too */
+  int32_t dxb;
+  const uint16_t *dxb_w[IDF_MAX_DEPTH];
 } IdfDenseBlock;
 
 /* Head epilogue target */
@@ -400,6 +405,23 @@ int idf_conv3x3_dx3(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, ui
                     int32_t N, float *d_out, int64_t ld_out, int32_t act, float slope,
                     uint32_t *d_flag, void *d_workspace, int64_t workspace_bytes,
                     const IdfDx3Head *head);
+
+/* The bf16 direct conv ("dxb", conv3_dx3.hip with one product per tap): the dx3 kernel's
+ * tiling, packing, split K and LDS-DMA over the block's bf16 shadow d_x16 (pixel-major,
+ * ld_x16 a multiple of 16, 16-B aligned; channels [C, round16(C)) finite -- they meet zero
+ * weights), v_mfma_f32_16x16x32_bf16 with fp32 accumulation, two taps per K=32 MFMA (5 MFMAs
+ * per 16 channels x 9 taps).  Outputs: fp32 to d_out (unless head->skip_f32) and bf16 (nearest
+ * even) into the shadow at channel C, zeros on to round16(C + N).  d_w: [ceil(C/16)][9 taps]
+ * [nf][16 out][16 ch] bf16, each slab padded to whole KiB (packing.py dxb_weights), nft = nf <=
+ * 3 (one output group).  Split K (the 8 x 8 level) as idf_conv3x3_dx3: the same workspace
+ * (idf_conv3x3_dx3_workspace), its counters zero at the launch.  Geometries:
+ * idf_conv3x3_dxb_supported (16-wide canvases and the 8 x 8 segments). */
+int idf_conv3x3_dxb_supported(int32_t H, int32_t W, int32_t N);
+int idf_conv3x3_dxb(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, uint16_t *d_x16,
+                    int64_t ld_x16, const uint16_t *d_w, int32_t nft, const float *d_b3,
+                    const float *d_vtap, int32_t ldv, const float *d_bfull, int32_t N,
+                    float *d_out, int64_t ld_out, int32_t act, float slope, void *d_workspace,
+                    int64_t workspace_bytes, const IdfDx3Head *head);
 
 /* The same folded 3x3 conv on bf16 MFMA (v_mfma_f32_16x16x32_bf16, fp32 accumulation).
  * The input is the bf16 shadow d_x16 of the fp32 feature columns (ld_x16 a multiple of 8,

@@ -402,8 +402,10 @@ def _codec_for(levels, family="x3", wx3=True):
     from types import SimpleNamespace
     from idfcodec.codec import ImageCodec
     c = ImageCodec.__new__(ImageCodec)
+    # an fp32 engine without dx3 weights (FlowEngine.can_run's rule for it)
     c.engine = SimpleNamespace(levels=[SimpleNamespace(z=z, h=h, w=w) for z, h, w in levels],
-                               conv_family=family, wx3=wx3)
+                               conv_family=family, wx3=wx3,
+                               can_run=lambda conv: conv == "f32" or (conv == "x3" and wx3))
     return c
 
 

@@ -51,6 +51,28 @@ def main():
     for s, e, n, q in seg:
         if "rans_decode_kernel" in n:
             print(f"  {(s - d0) / 1e6:7.3f} {(e - d0) / 1e6:7.3f}  ({(e - s) / 1e6:.3f} ms) q={q}")
+    # the encode before it: dequant .. the decode's first rANS launch (serial runs only)
+    eseg = [e for e in ev if a <= e[0] < d0]
+    e_end = max(e[1] for e in eseg)
+    busy = sorted((s, e) for s, e, _, _ in eseg)
+    covered, cs, ce = 0, busy[0][0], busy[0][1]
+    for s, e in busy[1:]:
+        if s > ce:
+            covered += ce - cs
+            cs, ce = s, e
+        else:
+            ce = max(ce, e)
+    covered += ce - cs
+    rans_e = [(s, e) for s, e, n, _ in eseg if "rans_encode_kernel" in n]
+    print(f"encode before it: {(e_end - a) / 1e6:.3f} ms to its last kernel end, GPU busy "
+          f"{covered / 1e6:.3f} ms; rANS encode launches: " +
+          ", ".join(f"{(s - a) / 1e6:.2f}-{(e - a) / 1e6:.2f}" for s, e in rans_e))
+    # per decode level: the last kernel of the decode before each rANS launch, the gap
+    conv = [e for e in seg if "conv3" in e[2]]
+    if conv:
+        print(f"decode: first conv {(conv[0][0] - d0) / 1e6:.3f} ms, last conv end "
+              f"{(max(e[1] for e in conv) - d0) / 1e6:.3f} ms, last kernel end "
+              f"{(max(e[1] for e in seg) - d0) / 1e6:.3f} ms")
 
 
 if __name__ == "__main__":

@@ -39,7 +39,7 @@ DEFAULT_BATCH = {"resflow-cond-imagenet64": 1024, "resflows_smallpatch_split": 8
                  "resflow-patches-vqvae": 32}
 
 
-PEAK_TFLOPS = {"bf16": 2500.0, "x3": 2500.0, "dx3": 2500.0, "dx3w16": 2500.0,
+PEAK_TFLOPS = {"bf16": 2500.0, "dxb": 2500.0, "x3": 2500.0, "dx3": 2500.0, "dx3w16": 2500.0,
                "f32": 157.3}  # MI355X_MICROARCH.md dense peaks
 
 
@@ -72,10 +72,12 @@ def flow_conv_roofline(codec, fl, img):
         L.idf_timer_destroy(timer)
     from idfcodec.engine import SPLIT_F16
     split = eng.wino and eng.conv_mode in SPLIT_F16
-    mode = "bf16" if eng.precision == "bf16" else (eng.conv_mode if split else "f32")
+    mode = eng.conv_mode if eng.precision == "bf16" else (eng.conv_mode if split else "f32")
     nd = [(l, len(b.dx3_w)) for l in range(eng.nsplit) for b in eng.couple[l] + [eng.prior[l]]]
     dx3_levels = sorted({eng.levels[l].h for l, n in nd if n and eng.dx3_layers(l, eng.prior[l].geom)})
     kern = {"bf16": "conv3_bf16_kernel (bf16 MFMA, f32 accumulate)",
+            "dxb": "conv3_dx3_kernel<..., true> (direct conv, one bf16 product per tap on bf16 "
+                   "MFMA, f32 accumulate, packed tiles)",
             "x3": "conv3_wino_kernel<..., true, ...> (Winograd, split-f16 products on f16 MFMA)",
             "f32": "conv3_wino_kernel (Winograd, f32 MFMA)"}.get(
         mode, "conv3_dx3_kernel (direct split-f16 products on f16 MFMA, packed tiles) at levels "
