@@ -744,9 +744,10 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
       }
       const int c = g.C + n0;  // split channel of v[0]; c % 4 == 0, so v stays in one slab
       if (row_ok && !(IDF_DX3_ABLATE & 128) && c < zend) {
-        if constexpr (BF) {  // the bf16 shadow, round to nearest even
+        if constexpr (BF) {  // the bf16 copy, round to nearest even
           typedef __bf16 b4 __attribute__((ext_vector_type(4)));
-          *(b4*)(xsb + pix * g.xs_pix + c * 2) = __builtin_convertvector(v, b4);
+          *(b4*)(xsb + (int64_t)(c >> 4) * g.xs_slab + pix * g.xs_pix + (c & 15) * 2) =
+              __builtin_convertvector(v, b4);
         } else {
           const e4 h = __builtin_convertvector(v, e4);
           const e4 l = __builtin_convertvector(v - __builtin_convertvector(h, d4), e4);
@@ -846,6 +847,25 @@ __global__ void __launch_bounds__(256) dx3_split_cols_kernel(int64_t P, int32_t 
   const bool ok = fabsf(v[0]) < kDxInGuard && fabsf(v[1]) < kDxInGuard &&
                   fabsf(v[2]) < kDxInGuard && fabsf(v[3]) < kDxInGuard;
   if (!ok && flag) atomicOr(flag, 1u);
+}
+
+// Block-input bf16 copy for the bf16 direct conv: XB channels [c0, c1) of every pixel, slab-major
+// [slab][P][16] bf16 (round to nearest even), zeros for [c1, round16(c1)).  One thread per
+// (pixel, 4 channels); threads [0, nzero) also clear zero[] (the split-K counters).
+__global__ void __launch_bounds__(256) dxb_cols_kernel(int64_t P, int32_t c0, int32_t c1,
+                                                       const float* __restrict__ x, int64_t ld_x,
+                                                       uint16_t* __restrict__ xb,
+                                                       uint32_t* __restrict__ zero, int32_t nzero) {
+  const int nq = ((c1 + 15) / 16 * 16 - c0) / 4;
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < nzero) zero[g] = 0u;
+  if (g >= P * nq) return;
+  const int64_t pix = g / nq;
+  const int c = c0 + 4 * (int)(g - pix * nq);
+  d4 v = d4{0.f, 0.f, 0.f, 0.f};
+  if (c < c1) v = *(const d4*)(x + pix * ld_x + c);
+  typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+  *(b4*)((char*)xb + ((int64_t)(c >> 4) * P + pix) * 32 + (c & 15) * 2) = __builtin_convertvector(v, b4);
 }
 
 // ---- geometry plan (host): how a (H, W, N) layer tiles, packs and splits.  A function of the
@@ -1185,16 +1205,38 @@ extern "C" int idf_conv3x3_dx3(void* stream, int32_t B, int32_t H, int32_t W, in
                  d_workspace, workspace_bytes, head);
 }
 
+extern "C" int64_t idf_dxb_bytes(int64_t P, int32_t channels) {
+  if (P < 0 || channels < 0) return -1;
+  return (int64_t)((channels + 15) / 16) * P * 32;
+}
+
+extern "C" int idf_dxb_cols(void* stream, int64_t P, int32_t c0, int32_t c1, const float* x,
+                            int64_t ld_x, uint16_t* xb, int32_t nslab_xb, uint32_t* d_zero,
+                            int32_t nzero) {
+  if (P < 0 || c1 < c0 || nzero < 0 || (nzero && !d_zero)) return IDF_ERR_ARG;
+  if (P == 0 || c1 == c0) {
+    if (nzero) return hipMemsetAsync(d_zero, 0, 4 * (size_t)nzero, (hipStream_t)stream) == hipSuccess
+                          ? IDF_OK : IDF_ERR_HIP;
+    return IDF_OK;
+  }
+  if (!x || !xb || (c0 & 15) || (c1 & 3) || (ld_x & 3) || (uintptr_t)x % 16) return IDF_ERR_ARG;
+  if ((c1 + 15) / 16 > nslab_xb) return IDF_ERR_ARG;
+  int64_t n = P * (((c1 + 15) / 16 * 16 - c0) / 4);
+  if (n < nzero) n = nzero;
+  hipLaunchKernelGGL(dxb_cols_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, P, c0, c1, x, ld_x, xb, d_zero, nzero);
+  return idf_last_error();
+}
+
 extern "C" int idf_conv3x3_dxb(void* stream, int32_t B, int32_t H, int32_t W, int32_t C,
-                               uint16_t* x16, int64_t ld_x16, const uint16_t* w, int32_t nft,
+                               uint16_t* xb, int32_t nslab_xb, const uint16_t* w, int32_t nft,
                                const float* b3, const float* vtap, int32_t ldv, const float* bfull,
                                int32_t N, float* out, int64_t ld_out, int32_t act, float slope,
                                void* d_workspace, int64_t workspace_bytes,
                                const IdfDx3Head* head) {
-  // the shadow's rows are whole 16-channel slabs, 16-B aligned; its outputs' slab must exist
-  if ((ld_x16 & 15) || (uintptr_t)x16 % 16 || (C + N + 15) / 16 * 16 > ld_x16) return IDF_ERR_ARG;
+  if ((uintptr_t)xb % 16) return IDF_ERR_ARG;
   const int64_t P = (int64_t)B * H * W;
-  return dx3_run(stream, true, B, H, W, C, x16, 2 * ld_x16, 32, P * ld_x16 * 2, (int32_t)(ld_x16 / 16),
+  return dx3_run(stream, true, B, H, W, C, xb, 32, P * 32, idf_dxb_bytes(P, 16 * nslab_xb), nslab_xb,
                  w, nft, 1.0f, b3, vtap, ldv, bfull, N, out, ld_out, act, slope, nullptr,
                  d_workspace, workspace_bytes, head);
 }

@@ -609,35 +609,29 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
   int64_t ld16 = 0;
   float* ws = tmp;
   int64_t ws_floats = P * ld_tmp;
-  // bf16 blocks on the bf16 direct conv (IdfDenseBlock.dxb, conv3_dx3.hip): every layer, by
-  // the level geometry alone; the split-K workspace after the shadow, its counters zeroed here
-  bool dxb = false;
+  // bf16 blocks on the bf16 direct conv (IdfDenseBlock.dxb, conv3_dx3.hip) -- every layer, by
+  // the level geometry alone -- keep a slab-major bf16 copy of their features instead, set up
+  // with the dx3 split copy below
+  const bool dxb = blk->bf16 && blk->fold && blk->dxb && blk->depth > 0 &&
+                   idf_conv3x3_dxb_supported(H, W, blk->g_pad);
   if (blk->bf16) {
     if (!blk->fold) return IDF_ERR_ARG;
-    dxb = blk->dxb && blk->depth > 0 && idf_conv3x3_dxb_supported(H, W, blk->g_pad);
     for (int i = 0; i < blk->depth; ++i) {
       if (!blk->wb16[i]) return IDF_ERR_ARG;
       if (dxb && !blk->dxb_w[i]) return IDF_ERR_ARG;
     }
+  }
+  if (blk->bf16 && !dxb) {
     // pitch a multiple of 64 channels: a pixel's 32-channel slab is one aligned 64-B run
     ld16 = ((int64_t)blk->k_in[blk->depth] + 63) / 64 * 64;
-    const int64_t sh = dxb ? (P * ld16 / 2 + 63) / 64 * 64 : (P * ld16 / 2 + 3) / 4 * 4;  // floats
-    if (sh > ws_floats || (dxb && (uintptr_t)tmp % 256)) return IDF_ERR_WORKSPACE;
+    const int64_t sh = (P * ld16 / 2 + 3) / 4 * 4;  // floats
+    if (sh > ws_floats) return IDF_ERR_WORKSPACE;
     f16 = (uint16_t*)tmp;
     ws = tmp + sh;
     ws_floats -= sh;
     const int c0 = blk->k_in[0];
-    // zeros on to the next 8 channels (conv3_bf16's k-blocks) / 16 (dxb's slabs)
-    int rc = idf_f32_to_bf16_cols(stream, P, c0, dxb ? (c0 + 15) / 16 * 16 : (c0 + 7) / 8 * 8,
-                                  feat, ld_feat, f16, ld16);
+    int rc = idf_f32_to_bf16_cols(stream, P, c0, (c0 + 7) / 8 * 8, feat, ld_feat, f16, ld16);
     if (rc) return rc;
-    if (dxb) {
-      const int64_t need = idf_conv3x3_dx3_workspace(B, H, W, blk->k_in[blk->depth - 1], blk->g_pad);
-      if (need < 0 || need > ws_floats * 4) return IDF_ERR_WORKSPACE;
-      if (need > 0 && hipMemsetAsync(ws, 0, (size_t)idf_conv3x3_dx3_counter_bytes(B, H, W, blk->g_pad),
-                                     s) != hipSuccess)
-        return IDF_ERR_HIP;
-    }
   }
   // dx3 blocks keep the split copy of their feature columns (conv3_dx3.hip) at the front of
   // tmp: the block input is split once here, every dx3 layer writes its outputs in both
@@ -650,6 +644,7 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
   for (int i = n_dx3; dx3 && i < blk->depth; ++i)
     if (blk->dx3_w[i]) return IDF_ERR_ARG;  // not a prefix
   dx3 = dx3 && n_dx3 > 0;
+  if (dxb) n_dx3 = blk->depth;  // below: "dx3" setup for either direct conv
   uint16_t* xs = nullptr;
   int32_t nslab_xs = 0;
   char* dws = nullptr;  // the dx3 layers' split-K counters and partial sums, after the copy
@@ -659,11 +654,11 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
     const int nft = (blk->g_pad + 15) / 16, nf = nft < 4 ? nft : 4;
     return (nft + nf - 1) / nf * nf;
   }();
-  if (dx3) {
+  if (dx3 || dxb) {
     // the slabs the dx3 layers read: up to the last one's input (its own outputs are read by
     // no dx3 layer, so they are split only into the slab it reads)
     nslab_xs = (blk->k_in[n_dx3 - 1] + 15) / 16;
-    const int64_t xs_bytes = idf_dx3_split_bytes(P, 16 * nslab_xs);
+    const int64_t xs_bytes = dxb ? idf_dxb_bytes(P, 16 * nslab_xs) : idf_dx3_split_bytes(P, 16 * nslab_xs);
     const int64_t avail = ws_floats * 4;
     const int64_t off = (xs_bytes + 255) / 256 * 256;
     const int64_t need = idf_conv3x3_dx3_workspace(B, H, W, blk->k_in[n_dx3 - 1], blk->g_pad);
@@ -680,9 +675,12 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
       if (hoff + P * 64 <= avail) hacc = (float*)((char*)tmp + hoff);
     }
     const int64_t ctr = idf_conv3x3_dx3_counter_bytes(B, H, W, blk->g_pad);
-    int rc = idf_dx3_split_cols(stream, P, 0, blk->k_in[0], feat, ld_feat, xs, nslab_xs,
-                                blk->range_flag, need > 0 ? (uint32_t*)dws : nullptr,
-                                need > 0 ? (int32_t)(ctr / 4) : 0);
+    int rc = dxb ? idf_dxb_cols(stream, P, 0, blk->k_in[0], feat, ld_feat, xs, nslab_xs,
+                                need > 0 ? (uint32_t*)dws : nullptr,
+                                need > 0 ? (int32_t)(ctr / 4) : 0)
+                 : idf_dx3_split_cols(stream, P, 0, blk->k_in[0], feat, ld_feat, xs, nslab_xs,
+                                      blk->range_flag, need > 0 ? (uint32_t*)dws : nullptr,
+                                      need > 0 ? (int32_t)(ctr / 4) : 0);
     if (rc) return rc;
     if (hacc) {
       rc = idf_dx3_head_init(stream, P, blk->k_in[0], feat, ld_feat, blk->wh, blk->ldwh, blk->bh,
@@ -705,11 +703,11 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
       const bool wino = blk->wino && blk->wino_u[i] && idf_conv3x3_wino_supported(H, W);
       const bool bf = blk->bf16 != 0;
       const int n16 = (c + blk->g_pad + 7) / 8 * 8 - c;
-      int rc = (bf && dxb)
-                   ? idf_conv3x3_dxb(stream, B, H, W, c, f16, ld16, blk->dxb_w[i], dx3_nft,
+      int rc = dxb
+                   ? idf_conv3x3_dxb(stream, B, H, W, c, xs, nslab_xs, blk->dxb_w[i], dx3_nft,
                                      blk->b3[i], blk->vtap[i], blk->ldv, blk->bfull[i], blk->g_pad,
-                                     feat + c, ld_feat, blk->act, blk->slope, ws, ws_floats * 4,
-                                     nullptr)
+                                     feat + c, ld_feat, blk->act, blk->slope, dws, dws_bytes,
+                                     hacc ? &hd : nullptr)
                : bf
                    ? idf_conv3x3_bf16(stream, B, H, W, c, f16, ld16, blk->wb16[i], blk->g_alloc,
                                       blk->b3[i], blk->vtap[i], blk->ldv, blk->bfull[i],

@@ -129,8 +129,10 @@ SIGNATURES = {
     "idf_dx3_split_bytes": (i64, [i64, i32]),
     "idf_dx3_split_cols": (ctypes.c_int, [P, i64, i32, i32, P, i64, P, i32, P, P, i32]),
     "idf_conv3x3_dxb_supported": (ctypes.c_int, [i32, i32, i32]),
-    "idf_conv3x3_dxb": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, P, P, i32, P, i32,
+    "idf_conv3x3_dxb": (ctypes.c_int, [P, i32, i32, i32, i32, P, i32, P, i32, P, P, i32, P, i32,
                                        P, i64, i32, f32, P, i64, P]),
+    "idf_dxb_bytes": (i64, [i64, i32]),
+    "idf_dxb_cols": (ctypes.c_int, [P, i64, i32, i32, P, i64, P, i32, P, i32]),
     "idf_conv3x3_bf16_workspace": (i64, [i32, i32, i32, i32, i32]),
     "idf_conv3x3_bf16": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, P, i32, P, P, i32, P, i32,
                                         P, i64, P, i64, i32, i32, f32, P, i64]),

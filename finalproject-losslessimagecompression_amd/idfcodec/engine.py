@@ -136,6 +136,7 @@ class DeviceBlock:
         for i, u in enumerate(self.wb16):
             d.wb16[i] = u.data_ptr()
         d.dxb = 1 if (d.bf16 and self.dxb_w and DXB) else 0
+        d.fuse_head = 1 if ((d.dx3 or d.dxb) and HEAD_FUSE) else 0
         for i, u in enumerate(self.dxb_w):
             d.dxb_w[i] = u.data_ptr()
         d.ldv = packed.g_alloc
@@ -340,6 +341,7 @@ class FlowEngine:
                                  f"{BF16_MODES if self.dxb else ('bf16',)}, not {mode!r}")
             for b in self._blocks:
                 b.desc.dxb = 1 if (mode == "dxb" and b.dxb_w) else 0
+                b.desc.fuse_head = 1 if (b.desc.dxb and HEAD_FUSE) else 0
             self.conv_mode = mode
             return
         if mode not in CONV_MODES:

@@ -67,14 +67,11 @@ def dense_tmp(db: DeviceBlock, B: int, H: int, W: int, ld_tmp: int, device):
     split-K workspace where the geometry splits (idf_conv3x3_dx3_workspace)."""
     P = B * H * W
     n = P * ld_tmp
-    nd = len(db.dx3_w)
-    if nd and db.desc.dx3:  # + the split-K workspace and the fused head's sums [P][16]
+    # dx3 / dxb: + the split-K workspace and the fused head's sums [P][16]
+    nd = len(db.dx3_w) if db.desc.dx3 else (len(db.dxb_w) if db.desc.dxb else 0)
+    if nd:
         w = int(lib().idf_conv3x3_dx3_workspace(B, H, W, db.geom.k_in[nd - 1], db.geom.g_pad))
         n += (max(w, 0) + 512) // 4 + 32 * P
-    nb = len(db.dxb_w)
-    if nb and db.desc.dxb:  # + the bf16 direct conv's split-K workspace (after the shadow)
-        w = int(lib().idf_conv3x3_dx3_workspace(B, H, W, db.geom.k_in[nb - 1], db.geom.g_pad))
-        n += (max(w, 0) + 512) // 4 + 64
     tmp = torch.empty(n, dtype=torch.float32, device=device)
     return tmp, max(ld_tmp, (n // P) // 16 * 16)
 

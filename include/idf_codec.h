@@ -407,18 +407,23 @@ int idf_conv3x3_dx3(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, ui
                     const IdfDx3Head *head);
 
 /* The bf16 direct conv ("dxb", conv3_dx3.hip with one product per tap): the dx3 kernel's
- * tiling, packing, split K and LDS-DMA over the block's bf16 shadow d_x16 (pixel-major,
- * ld_x16 a multiple of 16, 16-B aligned; channels [C, round16(C)) finite -- they meet zero
- * weights), v_mfma_f32_16x16x32_bf16 with fp32 accumulation, two taps per K=32 MFMA (5 MFMAs
- * per 16 channels x 9 taps).  Outputs: fp32 to d_out (unless head->skip_f32) and bf16 (nearest
- * even) into the shadow at channel C, zeros on to round16(C + N).  d_w: [ceil(C/16)][9 taps]
- * [nf][16 out][16 ch] bf16, each slab padded to whole KiB (packing.py dxb_weights), nft = nf <=
- * 3 (one output group).  Split K (the 8 x 8 level) as idf_conv3x3_dx3: the same workspace
- * (idf_conv3x3_dx3_workspace), its counters zero at the launch.  Geometries:
+ * tiling, packing, split K and LDS-DMA over the block's bf16 copy XB = [nslab_xb][P][16 ch]
+ * bf16 (slab-major like the split copy, 32 B per pixel and slab; idf_dxb_bytes), written by
+ * idf_dxb_cols (the block input: bf16 nearest even, zeros for [c1, round16(c1)); also clears
+ * d_zero[0, nzero), the split-K counters) and by every dxb layer;
+ * v_mfma_f32_16x16x32_bf16 with fp32 accumulation, two taps per K=32 MFMA (5 MFMAs per 16
+ * channels x 9 taps).  Outputs: fp32 to d_out (unless head->skip_f32) and bf16 into XB at
+ * channel C, zeros on to round16(C + N).  d_w: [ceil(C/16)][9 taps][nf][16 out][16 ch] bf16,
+ * each slab padded to whole KiB (packing.py dxb_weights), nft = nf <= 3 (one output group).
+ * Split K (the 8 x 8 level) and the fused head (IdfDx3Head) as idf_conv3x3_dx3: the same
+ * workspace (idf_conv3x3_dx3_workspace, counters zero at the launch).  Geometries:
  * idf_conv3x3_dxb_supported (16-wide canvases and the 8 x 8 segments). */
+int64_t idf_dxb_bytes(int64_t P, int32_t channels);
+int idf_dxb_cols(void *stream, int64_t P, int32_t c0, int32_t c1, const float *d_x, int64_t ld_x,
+                 uint16_t *d_xb, int32_t nslab_xb, uint32_t *d_zero, int32_t nzero);
 int idf_conv3x3_dxb_supported(int32_t H, int32_t W, int32_t N);
-int idf_conv3x3_dxb(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, uint16_t *d_x16,
-                    int64_t ld_x16, const uint16_t *d_w, int32_t nft, const float *d_b3,
+int idf_conv3x3_dxb(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, uint16_t *d_xb,
+                    int32_t nslab_xb, const uint16_t *d_w, int32_t nft, const float *d_b3,
                     const float *d_vtap, int32_t ldv, const float *d_bfull, int32_t N,
                     float *d_out, int64_t ld_out, int32_t act, float slope, void *d_workspace,
                     int64_t workspace_bytes, const IdfDx3Head *head);

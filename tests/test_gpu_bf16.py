@@ -125,8 +125,8 @@ def test_bf16_small_flow_round_trip_and_batch_invariance(H, growth, depth):
 
 
 def _run_dxb(X, Wt, b3, vt, bfull, B, H, W, C, N, act="ReLU"):
-    """idf_conv3x3_dxb (the bf16 direct conv) as a DenseBlock runs it: the bf16 shadow
-    (pixel-major, zeros from C to the next 16 channels) poisoned past the columns the layer
+    """idf_conv3x3_dxb (the bf16 direct conv) as a DenseBlock runs it: the slab-major bf16 copy
+    (idf_dxb_cols: zeros from C to the next 16 channels) poisoned past the columns the layer
     may write, the split-K workspace zeroed."""
     from idfcodec import _lib
     from idfcodec._lib import check, lib, ptr
@@ -141,19 +141,23 @@ def _run_dxb(X, Wt, b3, vt, bfull, B, H, W, C, N, act="ReLU"):
     P = B * H * W
     out = torch.zeros(P, ld, device=dev)
     z = round_up(C + N, 16)
-    ld16 = z + 16
-    x16 = torch.full((P, ld16), 0x7FC0, dtype=torch.int16, device=dev)
-    check(lib().idf_f32_to_bf16_cols(_lib.stream_ptr(), P, C, round_up(C, 16), ptr(Xd), ld,
-                                     ptr(x16), ld16), "to bf16")
+    nslab = z // 16 + 1
+    assert lib().idf_dxb_bytes(P, 16 * nslab) == nslab * P * 32
+    xb = torch.full((nslab, P, 16), 0x7FC0, dtype=torch.int16, device=dev)
+    check(lib().idf_dxb_cols(_lib.stream_ptr(), P, 0, C, ptr(Xd), ld, ptr(xb), nslab, None, 0),
+          "to bf16")
     wsn = int(lib().idf_conv3x3_dx3_workspace(B, H, W, C, N))
     ws = torch.zeros(max(wsn, 256) // 4, dtype=torch.int32, device=dev)
-    check(lib().idf_conv3x3_dxb(_lib.stream_ptr(), B, H, W, C, ptr(x16), ld16, ptr(wd),
+    check(lib().idf_conv3x3_dxb(_lib.stream_ptr(), B, H, W, C, ptr(xb), nslab, ptr(wd),
                                 n_alloc // 16, ptr(b3d), ptr(vtd), n_alloc, ptr(bfd), N, ptr(out),
                                 ld, _lib.ACT[act], 0.01, ptr(ws), wsn, None), "dxb conv")
     torch.cuda.synchronize()
     if wsn:
         ctr = int(lib().idf_conv3x3_dx3_counter_bytes(B, H, W, N))
         assert not ws[:ctr // 4].any(), "dxb left a split-K counter non-zero"
+    x16 = xb.permute(1, 0, 2).reshape(P, nslab * 16)  # pixel-major view of the slab-major copy
+    xin = X[:, :C].to(torch.bfloat16).view(torch.int16)
+    assert torch.equal(x16[:, :C].cpu(), xin), "bf16 copy of the input differs"
     sh = x16[:, C:z].cpu()
     want = out[:, :N].cpu().to(torch.bfloat16).view(torch.int16)
     assert torch.equal(sh[:, :N], want), "bf16 shadow of the output differs"

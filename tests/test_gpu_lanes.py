@@ -205,17 +205,20 @@ def test_encode_fallback_beside_decode_exact(monkeypatch):
 @pytest.mark.parametrize("name,lvl,which", [("resflow-patches-vqvae", 0, "coupling"),
                                             ("resflow-patches-vqvae", 0, "prior"),
                                             ("resflows_smallpatch_split", 0, "coupling"),
-                                            ("resflows_smallpatch_split", 1, "coupling")])
+                                            ("resflows_smallpatch_split", 1, "coupling"),
+                                            ("resflow-cond-imagenet64", 0, "coupling")])
 def test_fused_blocks_two_streams(name, lvl, which):
     """A dense block with the fused head (dx3 layers + idf_dx3_head_init) run on two HIP streams
     at once, each on its own workspace, gives the bits it gives alone: what two decode lanes
     do.  (A head init staging its weights in LDS diverged here in 5-20 of 40 runs.)"""
     from idfcodec import _lib, configs, synthetic
     from idfcodec._lib import IdfHeadOut, ptr
-    eng = synthetic.build_model(configs.get(name)).cuda().engine()
+    model = synthetic.build_model(configs.get(name)).cuda()
+    model.idf_precision = configs.PRECISION.get(name, "f32")  # config 3: bf16 (dxb)
+    eng = model.engine()
     Lv = eng.levels[lvl]
     blk = eng.couple[lvl][0] if which == "coupling" else eng.prior[lvl]
-    assert blk.desc.fuse_head == 1 and blk.desc.dx3 == 1
+    assert blk.desc.fuse_head == 1 and (blk.desc.dx3 == 1 or blk.desc.dxb == 1)
     B = 64
     P = B * Lv.h * Lv.w
     k0 = blk.geom.k_in[0]

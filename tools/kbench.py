@@ -1,7 +1,7 @@
 """Kernel microbenchmark of the folded 3x3 conv at the imagenet64 shapes (B=256): the LDS
 halo-tiled kernel (idf_conv3x3_halo) and the implicit-GEMM kernel (idf_conv3x3_fold_f32),
 per level and layer width.  Prints achieved TFLOP/s (unpadded FLOPs).
-Env filters: KB_ONLY=wino,wx3,dx3,halo,gemm,bf16  KB_LEVELS=0,1,2  KB_LAYERS=0,3,6,9,11  KB_REPS=10."""
+Env filters: KB_ONLY=wino,wx3,dx3,halo,gemm,bf16,dxb  KB_LEVELS=0,1,2  KB_LAYERS=0,3,6,9,11  KB_REPS=10."""
 import os
 import sys
 
@@ -140,13 +140,33 @@ def main():
                                              ptr(feat) + c_pad * 4, ld, ptr(f16) + c_pad * 2, ld16,
                                              n16, 0, 0.0, ptr(bws), bwn), "bf16")
 
+            from idfcodec.packing import dxb_weights
+            WDB = torch.from_numpy(dxb_weights(np.random.default_rng(1).normal(
+                0, 0.01, (g_alloc, 9, ldw)).astype(np.float32), c_pad).view(np.int16)).to(dev)
+            nsb = (c_pad + g_pad + 15) // 16
+            fb = None
+            xwn, xws = 0, None
+            if "dxb" in only:
+                fb = torch.zeros(nsb * P * 16, dtype=torch.int16, device=dev)
+                check(lib().idf_dxb_cols(s, P, 0, c_pad, ptr(feat), ld, ptr(fb), nsb, None, 0),
+                      "to bf16")
+                xwn = int(lib().idf_conv3x3_dx3_workspace(B, hw, hw, c_pad, g_pad))
+                if xwn > 0:
+                    xws = torch.zeros(xwn // 4, dtype=torch.int32, device=dev)
+
+            def dxb():
+                check(lib().idf_conv3x3_dxb(s, B, hw, hw, c_pad, ptr(fb), nsb, ptr(WDB),
+                                            g_alloc // 16, ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
+                                            ptr(feat) + c_pad * 4, ld, 0, 0.0, ptr(xws), xwn, None),
+                      "dxb")
+
             def gemm():
                 check(lib().idf_conv3x3_fold_f32(s, B, hw, hw, c_pad, ptr(feat), ld, ptr(w), ldw,
                                                  g_alloc, ptr(b3), ptr(vt), g_alloc, ptr(b3), g_pad,
                                                  ptr(feat) + c_pad * 4, ld, 0, 0.0), "gemm")
             line = f"L{lvl} hw={hw:2d} c={c_pad:4d} P={P:7d}"
             for name, fn in (("wino", wino), ("wx3", wx3), ("dx3", dx3), ("dx3r4", dx3r4),
-                             ("halo", halo), ("gemm", gemm), ("bf16", bf16)):
+                             ("halo", halo), ("gemm", gemm), ("bf16", bf16), ("dxb", dxb)):
                 if name not in only:
                     continue
                 ms = time_it(fn, reps)
