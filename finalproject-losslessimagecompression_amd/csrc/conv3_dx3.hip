@@ -187,9 +187,9 @@ __device__ unsigned long long g_dx3_tl[4096][8];
 constexpr int kDxWaves = IDF_DX3_WAVES;
 constexpr int kDxThreads = 64 * kDxWaves;
 constexpr uint32_t kDxInvalid = 0xFFFFFFF0u;
-// slab-0 offset of an out-of-image halo slot: with the split buffer under 2 GiB (checked on the
-// host) kDxOff + s * slab stride lies past the buffer's end for every slab s, so the load
-// returns zeros
+// offset of an out-of-image halo slot: the halo DMA addresses one slab per buffer resource and
+// a slab is under 2 GiB (checked on the host), so kDxOff lies past its end and the load returns
+// zeros
 constexpr uint32_t kDxOff = 0x80000000u;
 // the split-f16 range guard on stored outputs: |y| < 8192, as wx3 (|x| < 32768 on block inputs
 // is checked where the inputs are split, idf_dx3_split_cols)
@@ -292,10 +292,9 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   // (2 PLANE_KIB), plane (k / PLANE_KIB) % 2, canvas slots 32 (k % PLANE_KIB) .. +31 (lane:
   // slot + lane / 2, 8 channels (lane & 1)); weight pieces: 1 KiB of the slab's group weights.
   const int64_t plane_b = g.P * 32;                      // bytes of one plane of one slab
-  const uint32_t xs_stride = (uint32_t)g.xs_slab;        // bytes per slab
-  const int64_t xs_bytes = g.xs_bytes;
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)g.xs, 0, (int)(xs_bytes < (int64_t)kDxInvalid ? xs_bytes : (int64_t)kDxInvalid), 0x00020000);
+  // the halo DMA addresses one slab at a time (a buffer resource per slab: 32-bit offsets
+  // within a slab, so the whole copy may exceed 4 GiB -- config 5's 2048-patch batches)
+  const int xs_rec = (int)(g.xs_slab < (int64_t)kDxInvalid ? g.xs_slab : (int64_t)kDxInvalid);
   const uint32_t wslab = (uint32_t)(g.ngroup * L::WST);  // weight bytes per slab
   const int64_t wbytes = (int64_t)g.nslab * wslab;
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
@@ -362,8 +361,9 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
     if (halo ? (IDF_DX3_ABLATE & 1) : (IDF_DX3_ABLATE & 4)) return;
     // one call site for both kinds of piece (the LDS address formed from the __shared__ array
     // itself): the host pass of hipcc drops the kernel's launch stub otherwise
-    const uint32_t off = pbase[i] + (halo ? (uint32_t)s * xs_stride
-                                          : (uint32_t)(s * g.ngroup) * (uint32_t)L::WST);
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)g.xs + (int64_t)s * g.xs_slab), 0, xs_rec, 0x00020000);
+    const uint32_t off = pbase[i] + (halo ? 0u : (uint32_t)(s * g.ngroup) * (uint32_t)L::WST);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(halo ? xr : wr,
                                              (dx_lds_ptr_t)(lds + st * L::STAGE + plo[i]), 16,
                                              off, 0, 0, 0);
@@ -1098,9 +1098,9 @@ static int dx3_run(void* stream, bool bf, int32_t B, int32_t H, int32_t W, int32
   if ((uintptr_t)out % 16 || ld_out % 4) return IDF_ERR_ARG;  // 16-B output stores
   if ((C + 15) / 16 > nslab_xs) return IDF_ERR_ARG;          // the input slabs must exist
   const int64_t P = (int64_t)B * H * W;
-  // 32-bit buffer offsets, and kDxOff past the end of every slab: the split buffer must span
-  // < 2 GiB (imagenet64's 32x32 level: B < ~960 images)
-  if (xs_bytes >= (int64_t)kDxOff) return IDF_ERR_UNSUPPORTED;
+  // 32-bit buffer offsets within a slab, and kDxOff past the end of every slab: one slab of the
+  // copy must span < 2 GiB (P < 32M pixels)
+  if (xs_slab >= (int64_t)kDxOff) return IDF_ERR_UNSUPPORTED;
   const int64_t nblk = (int64_t)sh.nblk_tiles * sh.pl.ngroup * sh.nchunk;
   if (sh.ntiles >= (1 << 20) || nblk >= (1 << 20)) return IDF_ERR_UNSUPPORTED;  // udiv_s operands
   Dx3Args g = {};

@@ -26,7 +26,7 @@ import torch
 
 from . import _lib
 from ._lib import IdfDenseBlock, IdfHeadOut, check, lib, ptr
-from .packing import PackedBlock, pack_dense_block, round_up
+from .packing import PackedBlock, pack_dense_block_cached, round_up
 
 FLOAT = 4
 CONV_MODES = ("dx3", "dx3w16", "x3", "f32")
@@ -252,12 +252,12 @@ class FlowEngine:
         self.ids = []
         self.inv_ids = []
         for l in range(self.nsplit):
-            self.couple.append([DeviceBlock(pack_dense_block(
+            self.couple.append([DeviceBlock(pack_dense_block_cached(
                 sd, f"blocks.{l}.flows.{2 * k + 1}.dense.", c_depth, c_act, fold=self.fold,
                 wino=self.wino, bf16=self.precision == "bf16", wx3=self.wx3,
                 dx3=self.dx3 and self._dx3_level(l), dx3_cmax=self._dx3_cmax(l)),
                 self.device) for k in range(self.nflows)])
-            self.prior.append(DeviceBlock(pack_dense_block(sd, f"blocks.{l}.prior.NN.", p_depth,
+            self.prior.append(DeviceBlock(pack_dense_block_cached(sd, f"blocks.{l}.prior.NN.", p_depth,
                                                            p_act, fold=self.fold, wino=self.wino,
                                                            bf16=self.precision == "bf16",
                                                            wx3=self.wx3,

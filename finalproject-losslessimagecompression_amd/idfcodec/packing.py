@@ -383,6 +383,45 @@ def pack_dense_block(sd: dict, prefix: str, depth: int, act: str = "ReLU",
                        n1s, ld1s, ld3s, nh_alloc, ldwh, wus, wbs, wxs, wys, wds, wdy, wdbs)
 
 
+# Packing a DenseBlock (float64 folds, Winograd / split / bf16 weight forms) costs ~0.4-1 s of
+# host time; an engine packs 27 of them for imagenet64.  Engines built from the same weights
+# (a test session building one seeded model many times, an encoder and a decoder in one
+# process) share the packed arrays: keyed by the block's parameter bytes and the packing
+# arguments, never mutated after packing.  IDF_PACK_CACHE=0 turns it off.
+_PACK_CACHE: "collections.OrderedDict" = None
+PACK_CACHE_MAX = 96
+
+
+def pack_dense_block_cached(sd: dict, prefix: str, depth: int, act: str = "ReLU", **kw):
+    """pack_dense_block, memoised on the content of the block's parameters under `prefix`."""
+    import collections
+    import hashlib
+    import os
+    global _PACK_CACHE
+    if os.environ.get("IDF_PACK_CACHE", "1") == "0":
+        return pack_dense_block(sd, prefix, depth, act, **kw)
+    if _PACK_CACHE is None:
+        _PACK_CACHE = collections.OrderedDict()
+    h = hashlib.blake2b(digest_size=20)
+    for k in sorted(k for k in sd if k.startswith(prefix)):
+        v = sd[k]
+        if hasattr(v, "detach"):
+            v = v.detach().cpu().contiguous().numpy()
+        a = np.ascontiguousarray(v)
+        h.update(k.encode() + b"\0" + str(a.dtype).encode() + str(a.shape).encode())
+        h.update(a.tobytes())
+    key = (h.hexdigest(), prefix, depth, act, tuple(sorted(kw.items())))
+    hit = _PACK_CACHE.get(key)
+    if hit is not None:
+        _PACK_CACHE.move_to_end(key)
+        return hit
+    pb = pack_dense_block(sd, prefix, depth, act, **kw)
+    _PACK_CACHE[key] = pb
+    while len(_PACK_CACHE) > PACK_CACHE_MAX:
+        _PACK_CACHE.popitem(last=False)
+    return pb
+
+
 def unpack_features(feat: np.ndarray, geom: BlockGeometry, n: int) -> np.ndarray:
     """Logical [P, n] view of the first n concatenated channels of a padded feature buffer."""
     return feat[:, geom.positions(n)]

@@ -439,3 +439,49 @@ def test_dx3_fused_head(B, H, W, nh, N):
         assert torch.equal(mean.view(B, nh // 2, H, W), h[:, :nh // 2])
         assert torch.equal(logs.view(B, nh // 2, H, W), h[:, nh // 2:])
         assert torch.allclose(scale, torch.exp(logs), rtol=1e-6, atol=0)
+
+
+def test_dx3_split_copy_over_2gib():
+    """A split copy larger than 2 GiB (config 5's 2048-patch batches have 2.8 GB): the halo DMA
+    addresses it a slab at a time; images at both ends of the batch equal the same images
+    alone."""
+    from idfcodec import _lib
+    from idfcodec._lib import check, lib, ptr
+    from idfcodec.packing import dx3_groups, dx3_weights
+    dev = torch.device("cuda")
+    B, H, W, C, N = 4400, 16, 16, 496, 44
+    P = B * H * W
+    ld = 560
+    nslab = (C + N + 15) // 16
+    assert lib().idf_dx3_split_bytes(P, 16 * nslab) > 2 ** 31
+    g = torch.Generator(device=dev).manual_seed(3)
+    X = torch.randn(P, ld, generator=g, device=dev)
+    gw = torch.Generator().manual_seed(4)
+    Wt = torch.randn(48, 9, C, generator=gw, dtype=torch.float64) / np.sqrt(9 * C)
+    Wt[N:] = 0.0
+    nf, ngroup = dx3_groups(48)
+    Wd, ysc = dx3_weights(Wt.numpy(), C)
+    Wdd = torch.from_numpy(Wd.view(np.int16)).to(dev)
+    b3 = (torch.randn(48, generator=gw) * 0.1).to(dev)
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    s = _lib.stream_ptr()
+
+    def run(Xin, Bn):
+        Pn = Bn * H * W
+        xs = torch.empty(nslab * 2 * Pn * 16, dtype=torch.int16, device=dev)
+        out = torch.zeros(Pn, ld, device=dev)
+        check(lib().idf_dx3_split_cols(s, Pn, 0, C, ptr(Xin), ld, ptr(xs), nslab, ptr(flag),
+                                       None, 0), "split")
+        check(lib().idf_conv3x3_dx3(s, Bn, H, W, C, ptr(xs), nslab, ptr(Wdd), nf * ngroup, ysc,
+                                    ptr(b3), None, 48, None, N, ptr(out), ld, _lib.ACT["ReLU"],
+                                    0.01, ptr(flag), None, 0, None), "dx3")
+        torch.cuda.synchronize()
+        del xs
+        return out[:, :N]
+
+    full = run(X, B)
+    hw = H * W
+    for i in (0, B - 1):
+        one = run(X[i * hw:(i + 1) * hw].contiguous(), 1)
+        assert torch.equal(full[i * hw:(i + 1) * hw], one), i
+    assert full.abs().sum() > 0
