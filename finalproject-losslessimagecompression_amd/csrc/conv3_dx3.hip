@@ -692,6 +692,23 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   const int zr = (g.C + g.N + 15) / 16 * 16, zend = zr < 16 * g.nslab_xs ? zr : 16 * g.nslab_xs;
   const bool lastg = grp == g.ngroup - 1;
   char* xsb = (char*)g.xs;
+  // the head's running sums of the wave's rows, loaded before any store of the epilogue (a
+  // store may alias them for all the compiler knows, so a load inside the row loop would wait
+  // out the previous rows' stores: one memory round trip per row)
+  d4 hprev[WR];
+#pragma unroll
+  for (int m = 0; m < WR; ++m) {
+    hprev[m] = d4{0.f, 0.f, 0.f, 0.f};
+    if (!fh) continue;
+    int iy = iyw, y = uyw + m - iyw * g.H;
+    if (g.gut) {
+      iy = udiv_s(uyw + m, g.hp);
+      y = uyw + m - iy * g.hp;
+    }
+    const int b_img = (dt.band * g.nby + iy) * g.nbx + ixj;
+    if (lane_ok && y < g.H && iy < g.nby && b_img < g.B && 4 * q < g.nh)
+      hprev[m] = *(const d4*)(g.hacc + (((int64_t)b_img * g.H + y) * g.Wd + xj) * 16 + 4 * q);
+  }
 #pragma unroll
   for (int m = 0; m < WR; ++m) {
     int iy = iyw, y = uyw + m - iyw * g.H;
@@ -775,7 +792,7 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
       }
       if (row_ok && 4 * q < g.nh) {
         d4* ap = (d4*)(g.hacc + pix * 16 + 4 * q);
-        const d4 prev = *ap;
+        const d4 prev = hprev[m];
         d4 hv;
 #pragma unroll
         for (int i = 0; i < 4; ++i) hv[i] = prev[i] + r4[i];
