@@ -260,6 +260,59 @@ __device__ __forceinline__ DxTile dx_tile(const Dx3Args& g, int tile) {
   return t;
 }
 
+// The epilogue's two LDS tables in one pass: the bias table [16 border classes][NF * 16]
+// (stage_bias's values: b3 plus the in-image taps' share of the folded 1x1 bias) and the fused
+// head's weights on this layer's outputs [16][NF * 16] (zeros past nh and past N).  Every global
+// load is issued before any is used -- one memory round trip per wave; a table row per round
+// trip queued behind the first slab's DMA and held the first barrier back by ~3k cycles.
+template <int NF>
+__device__ __forceinline__ void dx3_stage_tables(float* btab, float* htab, const Dx3Args& g,
+                                                 int grp, int tid) {
+  constexpr int NN = NF * 16, NE = 16 * NN;  // entries per table
+  constexpr int PER = (2 * NE + kDxThreads - 1) / kDxThreads;
+  const bool fold = g.vtap != nullptr, head = g.nh > 0;
+  float t[PER][11];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {  // entry e: bias entries [0, NE), head entries [NE, 2 NE)
+    const int e = tid + i * kDxThreads;  // (NE is a multiple of 256: the kind is wave-uniform)
+    const int eh = e < NE ? e : e - NE;
+    const int cls = eh / NN, n = grp * NN + eh - cls * NN;
+    const int nc = n < g.N ? n : 0;
+    if (e < NE) {
+      t[i][0] = g.b3[nc];
+      if (fold) {
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) t[i][1 + tap] = g.vtap[tap * g.ldv + nc];
+        t[i][10] = g.bfull[nc];
+      }
+    } else if (e < 2 * NE && head) {
+      t[i][0] = g.hw[(int64_t)(cls < g.nh ? cls : 0) * g.ldhw + g.C + nc];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = tid + i * kDxThreads;
+    const int eh = e < NE ? e : e - NE;
+    const int cls = eh / NN, n = grp * NN + eh - cls * NN;
+    if (e < NE) {
+      float v = t[i][0];
+      if (fold) {
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+          const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+          const bool ok = !((dy < 0 && (cls & 1)) || (dy > 0 && (cls & 2)) ||
+                            (dx < 0 && (cls & 4)) || (dx > 0 && (cls & 8)));
+          v = ok ? v + t[i][1 + tap] : v;
+        }
+        v = cls == 0 ? t[i][10] : v;
+      }
+      btab[eh] = n < g.N ? v : 0.0f;
+    } else if (e < 2 * NE && head) {
+      htab[eh] = (cls < g.nh && n < g.N) ? t[i][0] : 0.0f;
+    }
+  }
+}
+
 template <int NF, int WR, int PITCH, int PLANE_KIB, bool BF>
 __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   using L = Dx3Lds<NF, WR, PITCH, PLANE_KIB, BF>;
@@ -380,16 +433,7 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   for (int e = tid; e < NF * 512 / 16; e += kDxThreads) *(d4*)(lds + L::ZOFF + 16 * e) = d4{0.f, 0.f, 0.f, 0.f};
   DX3_PHASE(0, __builtin_amdgcn_s_memtime());
   DX3_PHASE(4, __builtin_amdgcn_s_memrealtime());
-  stage_bias((float*)(lds + L::BOFF), NF * 16, grp * NF * 16, g.N, g.b3, g.vtap, g.bfull, g.ldv,
-             tid, kDxThreads);
-  if (g.nh > 0) {  // the head's weights on this layer's output channels ([16][NF * 16], zeros
-                   // past nh and past the layer's N outputs)
-    float* htab = (float*)(lds + L::HOFF);
-    for (int e = tid; e < 16 * NF * 16; e += kDxThreads) {
-      const int o = e / (NF * 16), cc = e - o * (NF * 16), col = grp * NF * 16 + cc;
-      htab[e] = (o < g.nh && col < g.N) ? g.hw[(int64_t)o * g.ldhw + g.C + col] : 0.0f;
-    }
-  }
+  dx3_stage_tables<NF>((float*)(lds + L::BOFF), (float*)(lds + L::HOFF), g, grp, tid);
   DX3_PHASE(1, __builtin_amdgcn_s_memtime());
   DX3_TL(1);
 
@@ -692,39 +736,39 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   const int zr = (g.C + g.N + 15) / 16 * 16, zend = zr < 16 * g.nslab_xs ? zr : 16 * g.nslab_xs;
   const bool lastg = grp == g.ngroup - 1;
   char* xsb = (char*)g.xs;
+  // the wave's rows: image, y, pixel, whether the lane has an output there
+  int r_img[WR], r_y[WR];
+  int64_t r_pix[WR];
+  bool r_ok[WR];
+#pragma unroll
+  for (int m = 0; m < WR; ++m) {
+    int iy = iyw, y = uyw + m - iyw * g.H;
+    if (g.gut) {
+      iy = udiv_s(uyw + m, g.hp);
+      y = uyw + m - iy * g.hp;
+    }
+    r_img[m] = (dt.band * g.nby + iy) * g.nbx + ixj;
+    r_y[m] = y;
+    r_ok[m] = lane_ok && y < g.H && iy < g.nby && r_img[m] < g.B;
+    r_pix[m] = ((int64_t)r_img[m] * g.H + y) * g.Wd + xj;
+  }
   // the head's running sums of the wave's rows, loaded before any store of the epilogue (a
-  // store may alias them for all the compiler knows, so a load inside the row loop would wait
-  // out the previous rows' stores: one memory round trip per row)
+  // store may alias them for all the compiler knows, so a load after one would wait it out)
   d4 hprev[WR];
 #pragma unroll
   for (int m = 0; m < WR; ++m) {
     hprev[m] = d4{0.f, 0.f, 0.f, 0.f};
-    if (!fh) continue;
-    int iy = iyw, y = uyw + m - iyw * g.H;
-    if (g.gut) {
-      iy = udiv_s(uyw + m, g.hp);
-      y = uyw + m - iy * g.hp;
-    }
-    const int b_img = (dt.band * g.nby + iy) * g.nbx + ixj;
-    if (lane_ok && y < g.H && iy < g.nby && b_img < g.B && 4 * q < g.nh)
-      hprev[m] = *(const d4*)(g.hacc + (((int64_t)b_img * g.H + y) * g.Wd + xj) * 16 + 4 * q);
+    if (fh && r_ok[m] && 4 * q < g.nh) hprev[m] = *(const d4*)(g.hacc + r_pix[m] * 16 + 4 * q);
   }
+  // outputs: bias, activation, the fp32 and split stores; acc[m][n] becomes the output (zeros
+  // past N), which the head's shares below read
 #pragma unroll
   for (int m = 0; m < WR; ++m) {
-    int iy = iyw, y = uyw + m - iyw * g.H;
-    if (g.gut) {
-      iy = udiv_s(uyw + m, g.hp);
-      y = uyw + m - iy * g.hp;
-    }
-    const int b_img = (dt.band * g.nby + iy) * g.nbx + ixj;
-    const bool row_ok = lane_ok && y < g.H && iy < g.nby && b_img < g.B;
+    const bool row_ok = r_ok[m];
     if (!row_ok && !fh) continue;
-    const int cls = bias_class(y, xj, g.H, g.Wd);
-    const int64_t pix = ((int64_t)b_img * g.H + y) * g.Wd + xj;
+    const int cls = bias_class(r_y[m], xj, g.H, g.Wd);
+    const int64_t pix = r_pix[m];
     float* dst = g.out + pix * g.ldo;
-    float hp[16];  // this lane's share of the head sums of its pixel (its 4 x NF channels)
-#pragma unroll
-    for (int o = 0; o < 16; ++o) hp[o] = 0.0f;
 #pragma unroll
     for (int n = 0; n <= NF; ++n) {
       if (n == NF && !lastg) break;
@@ -749,16 +793,8 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
           }
         }
         for (int k = g.N - n0; k < 4; ++k) v[k] = 0.0f;
-        if (fh) {  // head share: channels in order, fragments in order (zero weights past N)
-#pragma unroll
-          for (int o = 0; o < 16; ++o) {
-            if (o >= g.nh) break;
-            const d4 wv = *(const d4*)(htab + o * (NF * 16) + nl);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) hp[o] = __builtin_fmaf(wv[k], v[k], hp[o]);
-          }
-        }
       }
+      if (n < NF) acc[m][n] = v;
       const int c = g.C + n0;  // split channel of v[0]; c % 4 == 0, so v stays in one slab
       if (row_ok && !(IDF_DX3_ABLATE & 128) && c < zend) {
         if constexpr (BF) {  // the bf16 copy, round to nearest even
@@ -774,14 +810,41 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
         }
       }
     }
-    if (fh) {
+  }
+  if (fh) {
+    // this lane's share of the head sums of its pixels (its 4 x NF channels): each head weight
+    // quad read from LDS once and applied to the wave's WR rows (per row and output: channels
+    // in order, fragments in order; zero weights past N) -- one read per row cost the epilogue
+    // ~8k cycles of LDS bandwidth per block
+    float hp[WR][16];
+#pragma unroll
+    for (int m = 0; m < WR; ++m)
+#pragma unroll
+      for (int o = 0; o < 16; ++o) hp[m][o] = 0.0f;
+#pragma unroll
+    for (int n = 0; n < NF; ++n) {
+      const int nl = 16 * n + 4 * q;
+      if (16 * grp * NF + nl >= g.N) continue;
+#pragma unroll
+      for (int o = 0; o < 16; ++o) {
+        if (o < g.nh) {  // (no early exit: the loop must unroll, hp stays in registers)
+          const d4 wv = *(const d4*)(htab + o * (NF * 16) + nl);
+#pragma unroll
+          for (int m = 0; m < WR; ++m)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) hp[m][o] = __builtin_fmaf(wv[k], acc[m][n][k], hp[m][o]);
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < WR; ++m) {
       // the pixel's 4 lanes (q) reduce-scatter their shares: lane q ends with the sums of head
       // outputs 4q .. 4q + 3 -- (h_q + h_q^2) then + the pair q^1 -- one fixed order per output
       float r8[8], r4[4];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const float mine = q < 2 ? hp[i] : hp[8 + i];
-        const float give = q < 2 ? hp[8 + i] : hp[i];
+        const float mine = q < 2 ? hp[m][i] : hp[m][8 + i];
+        const float give = q < 2 ? hp[m][8 + i] : hp[m][i];
         r8[i] = mine + __shfl_xor(give, 32);
       }
 #pragma unroll
@@ -790,7 +853,8 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
         const float give = (q & 1) ? r8[i] : r8[4 + i];
         r4[i] = mine + __shfl_xor(give, 16);
       }
-      if (row_ok && 4 * q < g.nh) {
+      if (r_ok[m] && 4 * q < g.nh) {
+        const int64_t pix = r_pix[m];
         d4* ap = (d4*)(g.hacc + pix * 16 + 4 * q);
         const d4 prev = hprev[m];
         d4 hv;
@@ -799,7 +863,8 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
         if (!g.hlast) {
           *ap = hv;
         } else {  // the complete head: its epilogue (flow_kernels.hip gemm_f32_kernel's)
-          const int64_t hw_ = (int64_t)g.H * g.Wd, rem = (int64_t)y * g.Wd + xj;
+          const int b_img = r_img[m];
+          const int64_t hw_ = (int64_t)g.H * g.Wd, rem = (int64_t)r_y[m] * g.Wd + xj;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int o = 4 * q + i;
