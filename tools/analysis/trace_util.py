@@ -4,7 +4,8 @@ A step runs from one dequant launch (the start of an encode) to the next.  Every
 taken to hold min(256, its workgroups) CUs while it runs (the convs run one 512-thread block
 per CU; the serial rANS passes a handful of waves per CU at most), and the timeline of the sum
 over concurrent kernels, capped at 256, gives the CU-time actually in use -- the share of the
-step each half (encode: up to the first rans_decode_prep launch; decode: the rest) leaves idle.
+step each half (encode: up to the first rans_decode_kernel launch; decode: the rest) leaves idle.
+Run it on a --pipeline 0 trace: pipelined steps overlap an encode with a decode.
 
 usage: python tools/analysis/trace_util.py run_kernel_trace.csv [step index, default 2]
 """
@@ -26,7 +27,7 @@ def main():
     a, b = marks[k], marks[k + 1]
     seg = [e for e in ev if a <= e[0] < b]
     pts = sorted([(s, c) for s, _, _, c in seg] + [(e, -c) for _, e, _, c in seg])
-    dp = min(e[0] for e in seg if "rans_decode_prep" in e[2])
+    dp = min(e[0] for e in seg if "rans_decode_kernel" in e[2])
 
     def util(x, y):
         cur, last, acc = 0, x, 0
