@@ -180,6 +180,15 @@ __device__ unsigned long long g_dx3_tl[4096][8];
 #define IDF_DX3_FORCE1 0
 #endif
 
+// the split slab schedule (see the kernel): 0 (the library's) [wh ; wh] . [xh | xl] per tap, 42
+// weight-fragment reads a slab and wave; 1 pairs the hi weights' taps as the lo weights' are, 30
+// reads at the same MFMA count -- L0 c = 496 1.4% faster, but its other summation order moves one
+// teacher-forced coupling rounding of the imagenet64 B = 16 fixture from level 2 to level 1, so
+// the latents differ from the reference's in 0 / 4 / 50 places instead of 0 / 0 / 0
+// (profiles/r05/pairs/); a timing A/B build only
+#ifndef IDF_DX3_PAIRS
+#define IDF_DX3_PAIRS 0
+#endif
 // waves per block (timing A/B: 16 = four per SIMD at 2 rows per wave)
 #ifndef IDF_DX3_WAVES
 #define IDF_DX3_WAVES 8
@@ -205,7 +214,8 @@ template <int NF, int WR, int PITCH, int PLANE_KIB, bool BF>
 struct Dx3Lds {
   static constexpr int T = WR * kDxWaves / 16;     // tiles per block
   static constexpr int HR = WR + 2;                // canvas rows a wave reads
-  static constexpr int NS = BF ? 2 * HR - 1 : 5 * HR - 1;  // steps per slab (the schedule)
+  // steps per slab (the schedule)
+  static constexpr int NS = BF ? 2 * HR - 1 : IDF_DX3_PAIRS ? 3 * HR - 1 + 2 * WR : 5 * HR - 1;
   static constexpr int NPL = BF ? 1 : 2;           // planes per tile canvas: xh, xl / x
   static constexpr int PLANE = PLANE_KIB * 1024;   // one plane (xh or xl) of a tile's canvas
   static constexpr int SLOTS = PLANE / 32;
@@ -472,6 +482,9 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   const int oAG = L::WOFF + WLO + 2 * NF * 512 + j * 32 + (q & 1) * 16 + (q >> 1) * 3 * NF * 512;
   // [0 ; wl(2, 2)]: + n * 512; lanes q < 2 read the zero block (outside the stages)
   const int oAO = L::WOFF + WLO + 8 * NF * 512 + j * 32 + (q & 1) * 16;
+  // [wh(dy, 0) ; wh(dy, 1)]: + (3 dy * NF + n) * 512, and [wh(0, 2) ; wh(1, 2)]: + n * 512
+  const int oAHF = L::WOFF + j * 32 + (q & 1) * 16 + (q >> 1) * NF * 512;
+  const int oAHG = L::WOFF + 2 * NF * 512 + j * 32 + (q & 1) * 16 + (q >> 1) * 3 * NF * 512;
   const bool zlane = q < 2;
   const char* zO = lds + L::ZOFF + j * 32 + (q & 1) * 16;
 
@@ -606,6 +619,93 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
         }
       };
       dx_unroll(stepb, std::make_integer_sequence<int, NS>{});
+      DX3_STAMP(s - s0, 3);
+      continue;
+    }
+    if constexpr (IDF_DX3_PAIRS) {
+      // The paired schedule: the hi weights' taps paired as the lo weights' are, so no weight
+      // fragment is read twice ([wh ; wh] was: 42 weight-fragment reads a slab, now 30 -- the
+      // CU's LDS read bandwidth co-bounds the loop), at the same 14 MFMAs per row and fragment:
+      //   F_h [0, HR)          h = t:            [wh(dy,0) ; wh(dy,1)], [wl(dy,0) ; wl(dy,1)]
+      //                                          . [xh(h,0) | xh(h,1)]
+      //   F_l [HR, 2HR)        h = t - HR:       [wh(dy,0) ; wh(dy,1)] . [xl(h,0) | xl(h,1)]
+      //   G_h [2HR, 3HR-1)     h = t - 2HR:      [wh(0,2) ; wh(1,2)], [wl(0,2) ; wl(1,2)] (row h),
+      //                                          [0 ; wl(2,2)] (row h - 1) . [xh(h,2) | xh(h+1,2)]
+      //   G_l [3HR-1, +WR)     h = t - 3HR + 1:  [wh(0,2) ; wh(1,2)] . [xl(h,2) | xl(h+1,2)]
+      //   P   [TP, NS)         m = t - TP:       [wh(2,2) ; wh(2,2)] . [xh | xl](m + 2, 2)
+      constexpr int TL = HR, TG = 2 * HR, TGL = 3 * HR - 1, TP = TGL + WR;
+      static_assert(BF || TP + WR == NS, "the paired schedule's steps");
+      e8 AH[3][NF], AL[3][NF], GH[NF], GL[NF], GZ[NF], PW[NF];
+      auto read_Bp = [&](const char* st, int t) -> e8 {
+        if (t < TL) return rdB(st + oF + t * PITCH * 32);
+        if (t < TG) return rdB(st + oF + L::PLANE + (t - TL) * PITCH * 32);
+        if (t < TGL) return rdB(st + oG + (t - TG) * PITCH * 32);
+        if (t < TP) return rdB(st + oG + L::PLANE + (t - TGL) * PITCH * 32);
+        return rdB(st + oP + ((t - TP + 2) * PITCH + 2) * 32);
+      };
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int n = 0; n < NF; ++n) AH[dy][n] = rdA(cur + oAHF + (3 * dy * NF + n) * 512);
+#pragma unroll
+      for (int n = 0; n < NF; ++n) AL[0][n] = rdA(cur + oAF + n * 512);
+#pragma unroll
+      for (int k = 0; k < DB; ++k) Bq[k] = read_Bp(cur, k);
+      auto stepp = [&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        if (IDF_DX3_SB) __builtin_amdgcn_sched_barrier(0);
+        dma_step(tc);
+        // weights one phase ahead where a register set is free: the lo F pairs dy = 1, 2 in steps
+        // 0, 1 (first used in steps 1, 2, after that step's hi products); the G sets in F_l
+        // (the lo F pairs are dead); the P set in G_h (the hi F pairs are dead)
+        if constexpr (t < 2) {
+#pragma unroll
+          for (int n = 0; n < NF; ++n) AL[t + 1][n] = rdA(cur + oAF + (3 * (t + 1) * NF + n) * 512);
+        }
+        if constexpr (t >= TL && t < TL + 3) {
+#pragma unroll
+          for (int n = 0; n < NF; ++n) {
+            if constexpr (t == TL) GH[n] = rdA(cur + oAHG + n * 512);
+            else if constexpr (t == TL + 1) GL[n] = rdA(cur + oAG + n * 512);
+            else GZ[n] = rdA(zlane ? zO + n * 512 : cur + oAO + n * 512);
+          }
+        }
+        if constexpr (t == TG) {
+#pragma unroll
+          for (int n = 0; n < NF; ++n) PW[n] = rdA(cur + oAH + (8 * NF + n) * 512);
+        }
+        if constexpr (t + DB < NS) Bq[(t + DB) % RB] = read_Bp(cur, t + DB);
+        const e8& Bv = Bq[t % RB];
+        if constexpr (t < TL) {
+          mma_rows(AH, Bv, t);
+          mma_rows(AL, Bv, t);
+        } else if constexpr (t < TG) {
+          mma_rows(AH, Bv, t - TL);
+        } else if constexpr (t < TGL) {
+          constexpr int h = t - TG;
+          if constexpr (h < WR) {
+#pragma unroll
+            for (int n = 0; n < NF; ++n) mma(GH[n], Bv, acc[h][n]);
+          }
+          if constexpr (h > 0) {
+#pragma unroll
+            for (int n = 0; n < NF; ++n) mma(GZ[n], Bv, acc[h - 1][n]);
+          }
+          if constexpr (h < WR) {
+#pragma unroll
+            for (int n = 0; n < NF; ++n) mma(GL[n], Bv, acc[h][n]);
+          }
+        } else if constexpr (t < TP) {
+          constexpr int h = t - TGL;
+#pragma unroll
+          for (int n = 0; n < NF; ++n) mma(GH[n], Bv, acc[h][n]);
+        } else {
+          constexpr int m = t - TP;
+#pragma unroll
+          for (int n = 0; n < NF; ++n) mma(PW[n], Bv, acc[m][n]);
+        }
+      };
+      dx_unroll(stepp, std::make_integer_sequence<int, NS>{});
       DX3_STAMP(s - s0, 3);
       continue;
     }
