@@ -175,6 +175,14 @@ __device__ unsigned long long g_dx3_tl[4096][8];
 #ifndef IDF_DX3_KSPLIT
 #define IDF_DX3_KSPLIT 4  // chunks of the split-K levels (timing A/B builds only: changes bits)
 #endif
+// split-K chunks at 16 x 16 (timing A/B builds only: changes bits)
+#ifndef IDF_DX3_KSPLIT16
+#define IDF_DX3_KSPLIT16 1
+#endif
+// two tiles per block from this many tiles up (every CU gets a block; timing A/B builds only)
+#ifndef IDF_DX3_TWO_MIN
+#define IDF_DX3_TWO_MIN 512
+#endif
 // 1: one tile per block at every geometry (timing A/B of the two block shapes)
 #ifndef IDF_DX3_FORCE1
 #define IDF_DX3_FORCE1 0
@@ -1102,7 +1110,8 @@ static Dx3Plan dx3_plan(int H, int W, int N) {
   }
   // split K where a level's tiles are few for any batch the bench runs (imagenet64's 8 x 8:
   // 64 tiles per 256 images): by the geometry alone
-  p.split = (H * W <= 64 && p.nbx * p.nby <= 4) ? IDF_DX3_KSPLIT : 1;
+  p.split = (H * W <= 64 && p.nbx * p.nby <= 4) ? IDF_DX3_KSPLIT
+            : (H == 16 && W == 16) ? IDF_DX3_KSPLIT16 : 1;
   return p;
 }
 
@@ -1148,7 +1157,7 @@ Dx3Launch dx3_launch_shape(int B, int H, int W, int C, int N) {
   s.nslab = (C + 15) / 16;
   s.chunk_slabs = s.nslab > 0 ? (s.nslab + s.pl.split - 1) / s.pl.split : 1;
   s.nchunk = s.nslab > 0 ? (s.nslab + s.chunk_slabs - 1) / s.chunk_slabs : 1;
-  const bool two = s.pl.pitch == 18 && s.pl.nf <= 3 && s.nchunk == 1 && s.ntiles >= 2 * 256 &&
+  const bool two = s.pl.pitch == 18 && s.pl.nf <= 3 && s.nchunk == 1 && s.ntiles >= IDF_DX3_TWO_MIN &&
                    !IDF_DX3_FORCE1;
   s.T = two ? 2 : 1;  // two tiles (4 rows per wave) or one (2 rows)
   s.nblk_tiles = (int)((s.ntiles + s.T - 1) / s.T);
