@@ -278,58 +278,67 @@ __device__ __forceinline__ DxTile dx_tile(const Dx3Args& g, int tile) {
   return t;
 }
 
-// The epilogue's two LDS tables in one pass: the bias table [16 border classes][NF * 16]
-// (stage_bias's values: b3 plus the in-image taps' share of the folded 1x1 bias) and the fused
-// head's weights on this layer's outputs [16][NF * 16] (zeros past nh and past N).  Every global
-// load is issued before any is used -- one memory round trip per wave; a table row per round
-// trip queued behind the first slab's DMA and held the first barrier back by ~3k cycles.
+// The epilogue's two LDS tables: the bias table [16 border classes][NF * 16] (stage_bias's
+// values: b3 plus the in-image taps' share of the folded 1x1 bias) and the fused head's weights
+// on this layer's outputs [16][NF * 16] (zeros past nh and past N).  load() issues every global
+// load at once (one memory round trip); the kernel calls it after the first slab's barrier and
+// store() after the second's, so the loads overlap the first slab's MFMAs instead of holding the
+// first barrier back (a slab barrier waits for every outstanding load, these included).
 template <int NF>
-__device__ __forceinline__ void dx3_stage_tables(float* btab, float* htab, const Dx3Args& g,
-                                                 int grp, int tid) {
-  constexpr int NN = NF * 16, NE = 16 * NN;  // entries per table
-  constexpr int PER = (2 * NE + kDxThreads - 1) / kDxThreads;
-  const bool fold = g.vtap != nullptr, head = g.nh > 0;
-  float t[PER][11];
+struct Dx3Tables {
+  static constexpr int NN = NF * 16, NE = 16 * NN;  // outputs of the group; entries per table
+  static constexpr int HPER = (NE + kDxThreads - 1) / kDxThreads;  // head entries per thread
+  float bt[11];     // thread n < NN: output n's b3, 9 tap biases and full bias (all 16 classes)
+  float ht[HPER];   // head entries tid, tid + kDxThreads, ...
+
+  __device__ __forceinline__ void load(const Dx3Args& g, int grp, int tid) {
+    const int n = grp * NN + tid, nc = n < g.N ? n : 0;
+    if (tid < NN) {
+      bt[0] = g.b3[nc];
+      if (g.vtap) {
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {  // entry e: bias entries [0, NE), head entries [NE, 2 NE)
-    const int e = tid + i * kDxThreads;  // (NE is a multiple of 256: the kind is wave-uniform)
-    const int eh = e < NE ? e : e - NE;
-    const int cls = eh / NN, n = grp * NN + eh - cls * NN;
-    const int nc = n < g.N ? n : 0;
-    if (e < NE) {
-      t[i][0] = g.b3[nc];
-      if (fold) {
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap) t[i][1 + tap] = g.vtap[tap * g.ldv + nc];
-        t[i][10] = g.bfull[nc];
+        for (int tap = 0; tap < 9; ++tap) bt[1 + tap] = g.vtap[tap * g.ldv + nc];
+        bt[10] = g.bfull[nc];
       }
-    } else if (e < 2 * NE && head) {
-      t[i][0] = g.hw[(int64_t)(cls < g.nh ? cls : 0) * g.ldhw + g.C + nc];
+    }
+    if (g.nh > 0) {
+#pragma unroll
+      for (int i = 0; i < HPER; ++i) {
+        const int e = tid + i * kDxThreads, o = e / NN, hn = grp * NN + e - o * NN;
+        if (e < NE) ht[i] = g.hw[(int64_t)(o < g.nh ? o : 0) * g.ldhw + g.C + (hn < g.N ? hn : 0)];
+      }
     }
   }
+
+  __device__ __forceinline__ void store(float* btab, float* htab, const Dx3Args& g, int grp,
+                                        int tid) const {
+    if (tid < NN) {
+      const int n = grp * NN + tid;
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int e = tid + i * kDxThreads;
-    const int eh = e < NE ? e : e - NE;
-    const int cls = eh / NN, n = grp * NN + eh - cls * NN;
-    if (e < NE) {
-      float v = t[i][0];
-      if (fold) {
+      for (int cls = 0; cls < 16; ++cls) {
+        float v = bt[0];
+        if (g.vtap) {
 #pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-          const int dy = tap / 3 - 1, dx = tap % 3 - 1;
-          const bool ok = !((dy < 0 && (cls & 1)) || (dy > 0 && (cls & 2)) ||
-                            (dx < 0 && (cls & 4)) || (dx > 0 && (cls & 8)));
-          v = ok ? v + t[i][1 + tap] : v;
+          for (int tap = 0; tap < 9; ++tap) {
+            const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+            const bool ok = !((dy < 0 && (cls & 1)) || (dy > 0 && (cls & 2)) ||
+                              (dx < 0 && (cls & 4)) || (dx > 0 && (cls & 8)));
+            v = ok ? v + bt[1 + tap] : v;
+          }
+          v = cls == 0 ? bt[10] : v;
         }
-        v = cls == 0 ? t[i][10] : v;
+        btab[cls * NN + tid] = n < g.N ? v : 0.0f;
       }
-      btab[eh] = n < g.N ? v : 0.0f;
-    } else if (e < 2 * NE && head) {
-      htab[eh] = (cls < g.nh && n < g.N) ? t[i][0] : 0.0f;
+    }
+    if (g.nh > 0) {
+#pragma unroll
+      for (int i = 0; i < HPER; ++i) {
+        const int e = tid + i * kDxThreads, o = e / NN, hn = grp * NN + e - o * NN;
+        if (e < NE) htab[e] = (o < g.nh && hn < g.N) ? ht[i] : 0.0f;
+      }
     }
   }
-}
+};
 
 template <int NF, int WR, int PITCH, int PLANE_KIB, bool BF>
 __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
@@ -451,7 +460,7 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   for (int e = tid; e < NF * 512 / 16; e += kDxThreads) *(d4*)(lds + L::ZOFF + 16 * e) = d4{0.f, 0.f, 0.f, 0.f};
   DX3_PHASE(0, __builtin_amdgcn_s_memtime());
   DX3_PHASE(4, __builtin_amdgcn_s_memrealtime());
-  dx3_stage_tables<NF>((float*)(lds + L::BOFF), (float*)(lds + L::HOFF), g, grp, tid);
+  Dx3Tables<NF> tabs;  // loaded in the first slab, stored in the second (or after the loop)
   DX3_PHASE(1, __builtin_amdgcn_s_memtime());
   DX3_TL(1);
 
@@ -563,6 +572,8 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
     if (!(IDF_DX3_ABLATE & 8)) __builtin_amdgcn_s_barrier();
     DX3_STAMP(s - s0, 1);
     if (s == s0) DX3_TL(2);
+    if (s == s0) tabs.load(g, grp, tid);
+    if (s == s0 + 1) tabs.store((float*)(lds + L::BOFF), (float*)(lds + L::HOFF), g, grp, tid);
     __builtin_amdgcn_sched_barrier(0);
     const bool more = s + 1 < s1;
     const int nst = (s + 1 - s0) & 1;
@@ -762,6 +773,13 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   }
   DX3_PHASE(2, __builtin_amdgcn_s_memtime());
   DX3_TL(3);
+  // the tables in LDS before any epilogue reads them: stored here when the loop had no second
+  // slab, and ordered by one more barrier when no slab barrier followed the store
+  if (s1 - s0 <= 1) {
+    if (s1 == s0) tabs.load(g, grp, tid);
+    tabs.store((float*)(lds + L::BOFF), (float*)(lds + L::HOFF), g, grp, tid);
+  }
+  if (s1 - s0 <= 2) __syncthreads();
 
   // ---- split K: every chunk's block stores its raw sums; the tile's last block to finish
   // adds them in chunk order (its own from registers -- the same bits) and runs the epilogue.
