@@ -181,11 +181,13 @@ def rans_roofline(trace, bs, steps):
 def conv_kernel_name(eng):
     from idfcodec import engine
     if eng.wino and eng.conv_mode == "dx3":
-        return ("conv3_dx3_kernel<3, ...> at the 32x32 and 16x16 levels: DenseLayer 3x3 conv "
-                "with the 1x1 folded in, direct form, split-f16 products over the block's split "
-                "feature copy (x = xh + xl written once by the producer, halos by LDS-DMA; "
-                "xh.wh + xl.wh + xh.wl on v_mfma_f32_16x16x32_f16, f32 accumulation); "
-                "conv3_wino_kernel<3, 448, true, ...> (+ split-K reduce) at 8x8")
+        return ("conv3_dx3_kernel<3, ...> at every level (16 x 16 tiles of the 32x32 and 16x16 "
+                "images; the 8x8 images packed 2 x 2 a tile, split K in 4 chunks summed by the "
+                "tile's last block): DenseLayer 3x3 conv with the 1x1 folded in, direct form, "
+                "split-f16 products over the block's split feature copy (x = xh + xl written once "
+                "by the producer, halos by LDS-DMA; xh.wh + xl.wh + xh.wl on "
+                "v_mfma_f32_16x16x32_f16, f32 accumulation), the DenseBlock head's share added in "
+                "the epilogue")
     if eng.wino and eng.conv_mode == "x3":
         return ("conv3_wino_kernel<3, 448, true, false> (+conv3_wino_reduce_kernel at 8x8): "
                 "DenseLayer 3x3 conv with the 1x1 folded in, Winograd F(2x2,3x3), split-f16 "
