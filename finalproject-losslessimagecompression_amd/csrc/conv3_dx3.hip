@@ -79,6 +79,8 @@ struct Dx3Args {
   int32_t seg, segw, nseg;  // segment stride and width (slots), segments per canvas
   int32_t gut, wp, hp;  // 1: gutter packing -- images at pitch wp = W + 1 across, hp = H + 1
                         // down, the zero row / column between two images shared by both
+  int32_t tilew, xskip; // packed columns per tile (16; 24 with xskip) and xskip: 2-wide images,
+                        // lane j at image j / 2's column j % 2 (no lane on a gutter column)
   // split K
   int32_t nchunk, chunk_slabs;
   float* part;          // [nblk_tiles][ngroup][nchunk][waves][WR][NF][64 lanes] d4
@@ -217,7 +219,8 @@ constexpr float kDxOutGuard = 8192.0f;
 // 11: one 16-wide tile of one image (18 x 18 halo); 10 / 13: 8-wide images, two segments of
 // 10 x 20 (2 x 2 images of 8 x 8); 6 / 19: 4-wide images, four segments of 6 x 24; 26 / 17:
 // widths with one image edge inside a tile (two segments side by side, the second 8 slots past
-// the first's last lane: colbase = j mod 8).
+// the first's last lane: colbase = j mod 8); 25 / 15: 2-wide images gutter packed with every
+// lane on an image column (xskip: 25 x 18 slots).
 template <int NF, int WR, int PITCH, int PLANE_KIB, bool BF>
 struct Dx3Lds {
   static constexpr int T = WR * kDxWaves / 16;     // tiles per block
@@ -268,7 +271,7 @@ __device__ __forceinline__ DxTile dx_tile(const Dx3Args& g, int tile) {
   q = udiv_s(q, g.tiles_x);
   const int ty = q - udiv_s(q, g.tiles_y) * g.tiles_y;
   t.band = udiv_s(q, g.tiles_y);
-  t.u0 = 16 * tx;
+  t.u0 = g.tilew * tx;
   t.ix0 = udiv_s(t.u0, g.Wd);
   t.xf0 = t.u0 - t.ix0 * g.Wd;
   t.u0y = 16 * ty;
@@ -469,12 +472,13 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   // (segments: its rows lie in one image)
   const int j = lane & 15, q = lane >> 4;
   const DxTile dt = dx_tile(g, tile < g.ntiles ? tile : 0);
-  const int uj = dt.u0 + j;
+  const int jx = g.xskip ? 3 * (j >> 1) + (j & 1) : j;  // lane j's packed column in the tile
+  const int uj = dt.u0 + jx;
   const int pw = g.gut ? g.wp : g.Wd;
   const int ixj = udiv_s(uj, pw);             // lane j's image column in the band
   const int xj = uj - ixj * pw;               // and its x (gutter packing: W = the gutter)
   const int kj = ixj - dt.ix0;                // its segment
-  const int colb = g.gut ? j : kj * g.seg + (kj ? j - (ixj * g.Wd - dt.u0) : j);
+  const int colb = g.gut ? jx : kj * g.seg + (kj ? j - (ixj * g.Wd - dt.u0) : j);
   const int uyw = dt.u0y + r0;
   int iyw = udiv_s(uyw, g.H);
   if (iyw > g.nby - 1) iyw = g.nby - 1;
@@ -1080,13 +1084,15 @@ __global__ void __launch_bounds__(256) dxb_cols_kernel(int64_t P, int32_t c0, in
 // image geometry, the output count and C only -- never of the batch -- so an encoder and its
 // decoder run every layer with the same tiles, chunks and summation order.
 struct Dx3Plan {
-  int ok, pitch, plane_kib, nbx, nby, ch, seg, segw, nseg, gut, wp, hp, nf, ngroup, split;
+  int ok, pitch, plane_kib, nbx, nby, ch, seg, segw, nseg, gut, wp, hp, nf, ngroup, split, tilew,
+      xskip;
 };
 
 static int dx3_gcd(int a, int b) { return b ? dx3_gcd(b, a % b) : a; }
 
-static Dx3Plan dx3_plan(int H, int W, int N) {
+static Dx3Plan dx3_plan(int H, int W, int N, bool bf = false) {
   Dx3Plan p = {};
+  p.tilew = 16;
   if (H < 1 || W < 1 || N < 1 || N > 1024) return p;
   const int nft = (N + 15) / 16;
   p.nf = nft <= 4 ? nft : 4;
@@ -1125,6 +1131,12 @@ static Dx3Plan dx3_plan(int H, int W, int N) {
     while (p.nby > 1 && p.nby * p.hp > 128) p.nby /= 2;
     p.pitch = 18; p.ch = 18; p.segw = 18; p.nseg = 1; p.seg = 0; p.plane_kib = 11;
     p.ok = 1;
+    if (W == 2 && !bf) {
+      // 2-wide images (config 4's 2 x 2 level): the 16 lanes on 8 images' real columns, not on
+      // 16 packed columns of which a third are gutters -- a tile spans 24 packed columns, its
+      // canvas 25 x 18 slots (lane j's column base 3 (j / 2) + j % 2); the rows stay packed
+      p.xskip = 1; p.tilew = 24; p.pitch = 25; p.segw = 25; p.plane_kib = 15;
+    }
   }
   // split K where a level's tiles are few for any batch the bench runs (imagenet64's 8 x 8:
   // 64 tiles per 256 images): by the geometry alone
@@ -1153,7 +1165,9 @@ extern "C" int idf_dx3_stamps(unsigned long long* host) {
 namespace {
 
 // tiles across / down one band of the plan's packing
-int dx3_tiles_x(const Dx3Plan& p, int W) { return (p.nbx * (p.gut ? p.wp : W) + 15) / 16; }
+int dx3_tiles_x(const Dx3Plan& p, int W) {
+  return (p.nbx * (p.gut ? p.wp : W) + p.tilew - 1) / p.tilew;
+}
 int dx3_tiles_y(const Dx3Plan& p, int H) { return (p.nby * (p.gut ? p.hp : H) + 15) / 16; }
 
 struct Dx3Launch {
@@ -1165,9 +1179,9 @@ struct Dx3Launch {
 
 // the launch shape of a layer: tiles, tiles per block (two where every CU still gets a block,
 // at the 16-wide canvas), split-K chunks and the workspace they need
-Dx3Launch dx3_launch_shape(int B, int H, int W, int C, int N) {
+Dx3Launch dx3_launch_shape(int B, int H, int W, int C, int N, bool bf = false) {
   Dx3Launch s = {};
-  s.pl = dx3_plan(H, W, N);
+  s.pl = dx3_plan(H, W, N, bf);
   if (!s.pl.ok || B < 1) return s;
   const int64_t nbands = (B + s.pl.nbx * s.pl.nby - 1) / (s.pl.nbx * s.pl.nby);
   const int tiles_x = dx3_tiles_x(s.pl, W), tiles_y = dx3_tiles_y(s.pl, H);
@@ -1286,7 +1300,7 @@ static bool dxb_plan_ok(const Dx3Plan& p) {
 }
 
 extern "C" int idf_conv3x3_dxb_supported(int32_t H, int32_t W, int32_t N) {
-  return dxb_plan_ok(dx3_plan(H, W, N)) ? 1 : 0;
+  return dxb_plan_ok(dx3_plan(H, W, N, true)) ? 1 : 0;
 }
 
 // One dx3 launch, split-f16 (bf = false: xs the split copy) or bf16 (bf = true: xs the bf16
@@ -1299,7 +1313,7 @@ static int dx3_run(void* stream, bool bf, int32_t B, int32_t H, int32_t W, int32
                    int64_t workspace_bytes, const IdfDx3Head* head) {
   if (B <= 0 || H <= 0 || W <= 0 || N <= 0) return IDF_OK;
   if (C <= 0 || (C & 3) || !w || !xs || !out || !b3) return IDF_ERR_ARG;
-  const Dx3Launch sh = dx3_launch_shape(B, H, W, C, N);
+  const Dx3Launch sh = dx3_launch_shape(B, H, W, C, N, bf);
   if (!sh.pl.ok || (bf && !dxb_plan_ok(sh.pl))) return IDF_ERR_UNSUPPORTED;
   // the weights hold exactly the kernel's fragments: ngroup groups of nf, nft = ngroup * nf
   if (nft != sh.pl.ngroup * sh.pl.nf) return IDF_ERR_ARG;
@@ -1331,6 +1345,7 @@ static int dx3_run(void* stream, bool bf, int32_t B, int32_t H, int32_t W, int32
   g.nblk_tiles = sh.nblk_tiles;
   g.ch = sh.pl.ch; g.seg = sh.pl.seg; g.segw = sh.pl.segw; g.nseg = sh.pl.nseg;
   g.gut = sh.pl.gut; g.wp = sh.pl.wp; g.hp = sh.pl.hp;
+  g.tilew = sh.pl.tilew; g.xskip = sh.pl.xskip;
   g.nchunk = sh.nchunk; g.chunk_slabs = sh.chunk_slabs;
   g.b3 = b3; g.vtap = vtap; g.bfull = bfull; g.ldv = ldv; g.act = act; g.slope = slope;
   g.out = out; g.ldo = ld_out; g.yscale = yscale; g.flag = d_flag;
@@ -1393,6 +1408,8 @@ static int dx3_run(void* stream, bool bf, int32_t B, int32_t H, int32_t W, int32
     IDF_DX3_NF(W2, 18, 11)
   } else if (sh.pl.pitch == 10) {
     IDF_DX3_NF(W2, 10, 13)
+  } else if (sh.pl.pitch == 25) {
+    IDF_DX3_NF(W2, 25, 15)
   } else {
     IDF_DX3_NF(W2, 6, 19)
   }

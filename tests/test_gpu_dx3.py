@@ -196,7 +196,12 @@ def got_nchw(out, cs):
     (1, 8, 40, 20, 44, "ReLU", True), (37, 2, 2, 24, 128, "ReLU", True),
     (5, 7, 7, 20, 44, "ReLU", True), (3, 12, 12, 36, 44, "LeakyReLU", True),
     (6, 4, 8, 40, 44, "ReLU", True), (2, 5, 8, 24, 44, "ReLU", True),
-    (2, 16, 8, 24, 44, "ReLU", True)])
+    (2, 16, 8, 24, 44, "ReLU", True),
+    # 2-wide images with every lane on an image column (xskip): config 4's 2x2 level at 64
+    # outputs, a batch over one 16 x 16 band (partial second band), odd heights, one row
+    (5, 2, 2, 100, 64, "ReLU", True), (300, 2, 2, 36, 44, "LeakyReLU", True),
+    (3, 5, 2, 20, 44, "ReLU", True), (4, 1, 2, 12, 16, "ReLU", True),
+    (9, 2, 2, 20, 12, "None", False)])
 def test_dx3_vs_fp64(B, H, W, C, N, act, fold):
     cs = make_case(B, H, W, C, N, fold)
     out, flag, xs, P, nslab = run_dx3(cs, act)
