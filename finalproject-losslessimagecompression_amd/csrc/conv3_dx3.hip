@@ -199,6 +199,13 @@ __device__ unsigned long long g_dx3_tl[4096][8];
 #ifndef IDF_DX3_PAIRS
 #define IDF_DX3_PAIRS 0
 #endif
+// wave priority schedule in the split slab loop (timing A/B builds only; 0: none)
+#ifndef IDF_DX3_PRIO
+#define IDF_DX3_PRIO 0
+#endif
+#ifndef IDF_DX3_PRIO_K
+#define IDF_DX3_PRIO_K 4
+#endif
 // waves per block (timing A/B: 16 = four per SIMD at 2 rows per wave)
 #ifndef IDF_DX3_WAVES
 #define IDF_DX3_WAVES 8
@@ -740,6 +747,18 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
       constexpr int t = decltype(tc)::value;
       if (IDF_DX3_SB) __builtin_amdgcn_sched_barrier(0);  // keep the schedule: steps do not mix
       if constexpr (t == 9) DX3_STAMP(s - s0, 2);
+      // timing knob: wave priority by step (1: the SIMD's two waves alternate the lead every
+      // step; 2: every IDF_DX3_PRIO_K steps; 3: the younger wave leads the slab's first half)
+      if constexpr (IDF_DX3_PRIO == 1) {
+        if (((t & 1) != 0) == ((wave & 4) != 0)) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      } else if constexpr (IDF_DX3_PRIO == 2) {
+        if (((t / IDF_DX3_PRIO_K) & 1) == ((wave >> 2) & 1)) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      } else if constexpr (IDF_DX3_PRIO == 3) {
+        if constexpr (t == 0) { if (wave & 4) __builtin_amdgcn_s_setprio(1); }
+        if constexpr (t == NS / 2) __builtin_amdgcn_s_setprio(0);
+      }
       dma_step(tc);
       // weights of the next phase, one kernel row per step, in the first three steps of the
       // phase before it (its register set was freed by the phase before that)
