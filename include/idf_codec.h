@@ -356,7 +356,8 @@ int idf_conv3x3_wx3_res(void *stream, int32_t B, int32_t H, int32_t W, int32_t C
  * last slab holds finite values).  Geometry (idf_conv3x3_dx3_supported: any H, W): 16 x 16
  * output tiles of W a multiple of 16; of 16 / W images across (W = 8 or 4; H = 2, 4, 8 also
  * stacked down) in canvas segments; of any other geometry "gutter-packed" -- images at pitch
- * W + 1 across and H + 1 down, one zero column / row shared by neighbours.
+ * W + 1 across and H + 1 down, one zero column / row shared by neighbours (W = 2: every lane
+ * on an image column, the gutters only in the canvas).
  * Where the tiles are few for any batch (H * W <= 64 with <= 4 images a tile: imagenet64's
  * 8 x 8 level) the slabs split into up to 4 fixed chunks whose partial sums the last block of
  * a tile adds in chunk order: then d_workspace (256-B aligned, idf_conv3x3_dx3_workspace bytes)
