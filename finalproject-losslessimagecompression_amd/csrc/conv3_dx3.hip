@@ -618,9 +618,10 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
         return rdB(st + oG + (t - HR) * PITCH * 32);
       };
 #pragma unroll
-      for (int dy = 0; dy < 3; ++dy) read_A(cur, 3, dy, AS[1][dy]);
-#pragma unroll
-      for (int k = 0; k < DB; ++k) Bq[k] = read_Bf(cur, k);
+      for (int k = 0; k < (DB > 3 ? DB : 3); ++k) {  // in the order the first steps use them
+        if (k < DB) Bq[k] = read_Bf(cur, k);
+        if (k < 3) read_A(cur, 3, k, AS[1][k]);
+      }
       auto stepb = [&](auto tc) {
         constexpr int t = decltype(tc)::value;
         if (IDF_DX3_SB) __builtin_amdgcn_sched_barrier(0);
@@ -739,10 +740,13 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
       DX3_STAMP(s - s0, 3);
       continue;
     }
+    // the slab's first reads interleaved in the order the first steps use them (step h needs
+    // kernel rows dy <= h and pixel fragment h): the first MFMA waits for two reads, not twelve
 #pragma unroll
-    for (int dy = 0; dy < 3; ++dy) read_A(cur, 0, dy, AS[0][dy]);
-#pragma unroll
-    for (int k = 0; k < DB; ++k) Bq[k] = read_B(cur, k);
+    for (int k = 0; k < (DB > 3 ? DB : 3); ++k) {
+      if (k < DB) Bq[k] = read_B(cur, k);
+      if (k < 3) read_A(cur, 0, k, AS[0][k]);
+    }
     auto step = [&](auto tc) {
       constexpr int t = decltype(tc)::value;
       if (IDF_DX3_SB) __builtin_amdgcn_sched_barrier(0);  // keep the schedule: steps do not mix
