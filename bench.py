@@ -53,8 +53,8 @@ PX_PER_IMG = 64 * 64
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=B_PER_GPU)
     ap.add_argument("--cpu-baseline-images", type=int, default=64)
     ap.add_argument("--cpu-baseline-runs", type=int, default=3)
@@ -687,7 +687,7 @@ def main():
     if args.pipeline:
         # the same steps back to back (untimed for `value`): what one batch costs alone
         pe = []
-        for _ in range(2):
+        for _ in range(4):
             pe.append(step())
         torch.cuda.synchronize()
         se = sum(a.elapsed_time(b) for *_, (a, b, c) in pe) / len(pe)
