@@ -576,10 +576,14 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
 
   for (int s = s0; s < s1; ++s) {
     const char* cur = lds + ((s - s0) & 1) * L::STAGE;
-    // this wave's DMA of slab s landed; after the barrier every wave's has, and every wave is
-    // done reading the other stage (slab s - 1)
+    // this wave's DMA of slab s landed (vmcnt: LDS-DMA is a vector-memory load) and its LDS
+    // writes -- the zero block, the epilogue tables -- are done (lgkmcnt); after the barrier every
+    // wave's are, and every wave is done reading the other stage (slab s - 1).  The hardware
+    // s_barrier waits for neither counter, and a wave's LDS write still in flight at the barrier
+    // can land after another SIMD's wave has read the slot (the round-5 fused-head divergence:
+    // tools/repro_lds/, DESIGN.md section 4 "LDS ordering audit").
     DX3_STAMP(s - s0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     if (!(IDF_DX3_ABLATE & 8)) __builtin_amdgcn_s_barrier();
     DX3_STAMP(s - s0, 1);
     if (s == s0) DX3_TL(2);
@@ -1270,6 +1274,7 @@ extern "C" int idf_dx3_split_cols(void* stream, int64_t P, int32_t c0, int32_t c
   return idf_last_error();
 }
 
+#ifndef IDF_HEAD_INIT_EXTERNAL  // tools/repro_lds builds link a variant head init instead
 // The fused head's running sums start from the block input: acc[p][o] = bias[o] + sum over
 // c < C0 of w[o][c] x[p][c] (c in order), o < n_head; 0 for n_head <= o < 16.  One thread per
 // pixel, scalar FMAs on the weights read from global memory (wave-uniform, cached).  A version
@@ -1315,6 +1320,7 @@ extern "C" int idf_dx3_head_init(void* stream, int64_t P, int32_t C0, const floa
                      (hipStream_t)stream, P, C0, x, ld_x, w, ldw, bias, n_head, acc);
   return idf_last_error();
 }
+#endif  // IDF_HEAD_INIT_EXTERNAL
 
 // the bf16 kernel's geometries: the 16-wide canvas (tiles and gutter packing) and the 8 x 8
 // level's segments, one output group of up to 3 fragments (the bf16 blocks' growth <= 48)
@@ -1349,6 +1355,10 @@ static int dx3_run(void* stream, bool bf, int32_t B, int32_t H, int32_t W, int32
   if (xs_slab >= (int64_t)kDxOff) return IDF_ERR_UNSUPPORTED;
   const int64_t nblk = (int64_t)sh.nblk_tiles * sh.pl.ngroup * sh.nchunk;
   if (sh.ntiles >= (1 << 20) || nblk >= (1 << 20)) return IDF_ERR_UNSUPPORTED;  // udiv_s operands
+  // split K: the kernel addresses the partial sums with 32-bit offsets through one buffer
+  // resource (kDxInvalid records at most), nblk blocks x fragments x 1 KiB
+  if (sh.nchunk > 1 && nblk * (int64_t)(kDxWaves * (16 / kDxWaves) * sh.pl.nf) * 1024 >= (int64_t)kDxInvalid)
+    return IDF_ERR_UNSUPPORTED;
   Dx3Args g = {};
   if (sh.nchunk > 1) {
     const int64_t cb = idf_conv3x3_dx3_counter_bytes(B, H, W, N);

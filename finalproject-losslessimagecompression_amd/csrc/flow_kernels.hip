@@ -595,6 +595,64 @@ static void timer_mark(IdfTimer* t, hipStream_t s, int tag, double flops, bool b
   }
 }
 
+// The dx3 / dxb layers' part of a DenseBlock's tmp (dense_block_run): the block's split (dx3) or
+// bf16 (dxb) feature copy at the front, its layers' split-K workspace after it (256-B aligned),
+// and -- when the head is fused (IdfDenseBlock.fuse_head, by the geometry alone: every layer on
+// the direct conv, one output group, n_head <= 16, a block input of <= 64 channels) -- the head's
+// running sums [P][16] f32 after that.  Whether the head is fused depends on the block and the
+// geometry only, never on the room in tmp: a caller's tmp too small for the sums is an error
+// (IDF_ERR_WORKSPACE), not a silent switch to the head GEMM, whose sums run in another order.
+struct Dx3TmpPlan {
+  bool dx3, dxb, fuse;
+  int n_dx3, nslab_xs;
+  int64_t xs_bytes, off, need, hoff, bytes;  // bytes: the whole part (0 without dx3 / dxb)
+};
+
+static int dx3_tmp_plan(const IdfDenseBlock* blk, int32_t B, int32_t H, int32_t W, bool head,
+                        Dx3TmpPlan* pl) {
+  *pl = {};
+  const int64_t P = (int64_t)B * H * W;
+  pl->dxb = blk->bf16 && blk->fold && blk->dxb && blk->depth > 0 &&
+            idf_conv3x3_dxb_supported(H, W, blk->g_pad);
+  // the layers with dx3 weights are a prefix (the narrow ones, packing.py pack_dense_block
+  // dx3_cmax); the rest run on wx3, whose workspace then reuses the copy
+  bool dx3 = blk->fold && blk->wx3 && blk->dx3 && !blk->bf16 &&
+             idf_conv3x3_dx3_supported(H, W, blk->g_pad);
+  int n_dx3 = 0;
+  while (dx3 && n_dx3 < blk->depth && blk->dx3_w[n_dx3]) ++n_dx3;
+  for (int i = n_dx3; dx3 && i < blk->depth; ++i)
+    if (blk->dx3_w[i]) return IDF_ERR_ARG;  // not a prefix
+  pl->dx3 = dx3 && n_dx3 > 0;
+  if (pl->dxb) n_dx3 = blk->depth;  // below: "dx3" setup for either direct conv
+  pl->n_dx3 = n_dx3;
+  if (!pl->dx3 && !pl->dxb) return IDF_OK;
+  const int nft = (blk->g_pad + 15) / 16, nf = nft < 4 ? nft : 4;
+  const int dx3_nft = (nft + nf - 1) / nf * nf;  // fragments the dx3 weights hold
+  // the slabs the dx3 layers read: up to the last one's input (its own outputs are read by
+  // no dx3 layer, so they are split only into the slab it reads)
+  pl->nslab_xs = (blk->k_in[n_dx3 - 1] + 15) / 16;
+  pl->xs_bytes = pl->dxb ? idf_dxb_bytes(P, 16 * pl->nslab_xs) : idf_dx3_split_bytes(P, 16 * pl->nslab_xs);
+  pl->off = (pl->xs_bytes + 255) / 256 * 256;
+  pl->need = idf_conv3x3_dx3_workspace(B, H, W, blk->k_in[n_dx3 - 1], blk->g_pad);
+  if (pl->need < 0) return IDF_ERR_UNSUPPORTED;
+  pl->bytes = pl->off + pl->need;
+  pl->fuse = head && blk->fuse_head && n_dx3 == blk->depth && blk->n_head <= 16 && dx3_nft <= 4 &&
+             blk->k_in[0] <= 64 && blk->depth > 0;
+  if (pl->fuse) {
+    pl->hoff = (pl->off + pl->need + 255) / 256 * 256;
+    pl->bytes = pl->hoff + P * 64;
+  }
+  return IDF_OK;
+}
+
+extern "C" int64_t idf_dense_block_dx3_tmp_bytes(const IdfDenseBlock* blk, int32_t B, int32_t H,
+                                                  int32_t W) {
+  if (!blk || blk->depth < 0 || blk->depth > IDF_MAX_DEPTH || B < 0 || H < 1 || W < 1) return -1;
+  Dx3TmpPlan pl;
+  if (dx3_tmp_plan(blk, B, H, W, true, &pl)) return -1;
+  return pl.bytes;
+}
+
 static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, int32_t H, int32_t W,
                            float* feat, int64_t ld_feat, float* tmp, int64_t ld_tmp,
                            const IdfHeadOut* head, IdfTimer* timer) {
@@ -612,8 +670,9 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
   // bf16 blocks on the bf16 direct conv (IdfDenseBlock.dxb, conv3_dx3.hip) -- every layer, by
   // the level geometry alone -- keep a slab-major bf16 copy of their features instead, set up
   // with the dx3 split copy below
-  const bool dxb = blk->bf16 && blk->fold && blk->dxb && blk->depth > 0 &&
-                   idf_conv3x3_dxb_supported(H, W, blk->g_pad);
+  Dx3TmpPlan pl;
+  if (int rc = dx3_tmp_plan(blk, B, H, W, head != nullptr, &pl)) return rc;
+  const bool dxb = pl.dxb;
   if (blk->bf16) {
     if (!blk->fold) return IDF_ERR_ARG;
     for (int i = 0; i < blk->depth; ++i) {
@@ -635,16 +694,9 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
   }
   // dx3 blocks keep the split copy of their feature columns (conv3_dx3.hip) at the front of
   // tmp: the block input is split once here, every dx3 layer writes its outputs in both
-  // forms.  The layers with dx3 weights are a prefix (the narrow ones, packing.py
-  // pack_dense_block dx3_cmax); the rest run on wx3, whose workspace then reuses the copy.
-  bool dx3 = blk->fold && blk->wx3 && blk->dx3 && !blk->bf16 &&
-             idf_conv3x3_dx3_supported(H, W, blk->g_pad);
-  int n_dx3 = 0;
-  while (dx3 && n_dx3 < blk->depth && blk->dx3_w[n_dx3]) ++n_dx3;
-  for (int i = n_dx3; dx3 && i < blk->depth; ++i)
-    if (blk->dx3_w[i]) return IDF_ERR_ARG;  // not a prefix
-  dx3 = dx3 && n_dx3 > 0;
-  if (dxb) n_dx3 = blk->depth;  // below: "dx3" setup for either direct conv
+  // forms (dx3_tmp_plan: the layout)
+  const bool dx3 = pl.dx3;
+  const int n_dx3 = pl.n_dx3;
   uint16_t* xs = nullptr;
   int32_t nslab_xs = 0;
   char* dws = nullptr;  // the dx3 layers' split-K counters and partial sums, after the copy
@@ -655,25 +707,14 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
     return (nft + nf - 1) / nf * nf;
   }();
   if (dx3 || dxb) {
-    // the slabs the dx3 layers read: up to the last one's input (its own outputs are read by
-    // no dx3 layer, so they are split only into the slab it reads)
-    nslab_xs = (blk->k_in[n_dx3 - 1] + 15) / 16;
-    const int64_t xs_bytes = dxb ? idf_dxb_bytes(P, 16 * nslab_xs) : idf_dx3_split_bytes(P, 16 * nslab_xs);
     const int64_t avail = ws_floats * 4;
-    const int64_t off = (xs_bytes + 255) / 256 * 256;
-    const int64_t need = idf_conv3x3_dx3_workspace(B, H, W, blk->k_in[n_dx3 - 1], blk->g_pad);
-    if (need < 0 || off + need > avail || (uintptr_t)tmp % 256) return IDF_ERR_WORKSPACE;
+    if (pl.bytes > avail || (uintptr_t)tmp % 256) return IDF_ERR_WORKSPACE;
+    nslab_xs = pl.nslab_xs;
+    const int64_t need = pl.need;
     xs = (uint16_t*)tmp;
-    dws = (char*)tmp + off;
+    dws = (char*)tmp + pl.off;
     dws_bytes = need;
-    // the fused head (IdfDenseBlock.fuse_head): every layer on dx3 in one output group, a
-    // head of <= 16 outputs over a block input of <= 64 channels; its running sums [P][16]
-    // after the split-K workspace
-    if (head && blk->fuse_head && n_dx3 == blk->depth && blk->n_head <= 16 && dx3_nft <= 4 &&
-        blk->k_in[0] <= 64 && blk->depth > 0) {
-      const int64_t hoff = (off + need + 255) / 256 * 256;
-      if (hoff + P * 64 <= avail) hacc = (float*)((char*)tmp + hoff);
-    }
+    if (pl.fuse) hacc = (float*)((char*)tmp + pl.hoff);
     const int64_t ctr = idf_conv3x3_dx3_counter_bytes(B, H, W, blk->g_pad);
     int rc = dxb ? idf_dxb_cols(stream, P, 0, blk->k_in[0], feat, ld_feat, xs, nslab_xs,
                                 need > 0 ? (uint32_t*)dws : nullptr,

@@ -96,6 +96,7 @@ SIGNATURES = {
     "idf_rans_cdf_selfcheck": (ctypes.c_int, [P, u64, u64, P]),
     "idf_rans_part1_selfcheck": (ctypes.c_int, [P, u64, u64, P]),
     "idf_dense_block_f32": (ctypes.c_int, [P, P, i32, i32, i32, P, i64, P, i64, P]),
+    "idf_dense_block_dx3_tmp_bytes": (i64, [P, i32, i32, i32]),
     "idf_timer_create": (P, [i32]),
     "idf_timer_destroy": (None, [P]),
     "idf_timer_reset": (None, [P]),

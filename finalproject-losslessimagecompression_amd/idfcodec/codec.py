@@ -31,7 +31,8 @@ FLAG_CONV_X3 = 1
 # must run the same one.  Version 1 wrote 0 both for exact-f32 Winograd and for every engine
 # that predates the field (halo / gemm / unfold / bf16): a version-1 file with flags 0 reads as
 # conv "unrecorded", which any engine but a split-f16 one may decode (the pre-field behaviour).
-# 6: round 4's dx3 (direct split-f16 only at widths a multiple of 16: engine mode 'dx3w16');
+# 6: round 4's dx3 (direct split-f16 only at widths a multiple of 16: engine mode 'dx3w16'; a
+#    file the round-4 build wrote decodes exactly today: tests/golden/imagenet64_code6_r4.npz);
 # 7: dx3 on every geometry conv3_dx3.hip packs (imagenet64's 8x8 level too); 8: bf16 engines on
 # the bf16 direct conv (engine mode 'dxb'; 5 = conv3_bf16.hip)
 CONV_CODES = {"f32": 0, "x3": 1, "halo": 2, "gemm": 3, "unfold": 4, "bf16": 5, "dx3w16": 6,

@@ -25,7 +25,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import IdfDenseBlock, IdfHeadOut, check, lib, ptr
+from ._lib import IdfDenseBlock, IdfError, IdfHeadOut, check, lib, ptr
 from .packing import PackedBlock, pack_dense_block_cached, round_up
 
 FLOAT = 4
@@ -56,10 +56,10 @@ DX3 = os.environ.get("IDF_DX3", "1") != "0"
 # outputs (every coupling, the 32x32 prior) fuses the head into its layers: running sums from
 # the block input (idf_dx3_head_init), each layer's epilogue adds its outputs' share, the last
 # applies the coupling / prior epilogue -- no head GEMM re-reading the feature buffer, and the
-# layers skip their fp32 output stores (IdfDenseBlock.fuse_head / keep_feat).  IDF_HEAD_FUSE=0
-# keeps the GEMM heads (timing A/B only: the head's sums run in another order, so encoder and
-# decoder must agree on it).
-HEAD_FUSE = os.environ.get("IDF_HEAD_FUSE", "1") != "0"
+# layers skip their fp32 output stores (IdfDenseBlock.fuse_head / keep_feat).  The fusion is part
+# of the conv arithmetic the mode names (the head's sums run in another order than the GEMM's):
+# on in modes 'dx3' and 'dxb', off in 'dx3w16', decided by the block geometry alone -- no switch,
+# so an encoder and its decoder cannot disagree on it.
 # bf16 engines (configs naming bf16 coupling convs) run their DenseLayers as the bf16 direct
 # conv (conv mode "dxb", idf_conv3x3_dxb: the dx3 kernel's tiling and LDS-DMA with one bf16
 # product per tap) where the level geometry allows, conv3_bf16.hip ("bf16", round 4's) elsewhere
@@ -127,7 +127,7 @@ class DeviceBlock:
             d.wx3_u[i] = u.data_ptr()
             d.wx3_yscale[i] = packed.wx3_yscale[i]
         d.dx3 = 1 if (d.wx3 and self.dx3_w) else 0
-        d.fuse_head = 1 if (d.dx3 and HEAD_FUSE) else 0
+        d.fuse_head = 1 if d.dx3 else 0
         d.keep_feat = 0
         for i, w in enumerate(self.dx3_w):
             d.dx3_w[i] = w.data_ptr()
@@ -136,7 +136,7 @@ class DeviceBlock:
         for i, u in enumerate(self.wb16):
             d.wb16[i] = u.data_ptr()
         d.dxb = 1 if (d.bf16 and self.dxb_w and DXB) else 0
-        d.fuse_head = 1 if ((d.dx3 or d.dxb) and HEAD_FUSE) else 0
+        d.fuse_head = 1 if (d.dx3 or d.dxb) else 0
         for i, u in enumerate(self.dxb_w):
             d.dxb_w[i] = u.data_ptr()
         d.ldv = packed.g_alloc
@@ -341,7 +341,7 @@ class FlowEngine:
                                  f"{BF16_MODES if self.dxb else ('bf16',)}, not {mode!r}")
             for b in self._blocks:
                 b.desc.dxb = 1 if (mode == "dxb" and b.dxb_w) else 0
-                b.desc.fuse_head = 1 if (b.desc.dxb and HEAD_FUSE) else 0
+                b.desc.fuse_head = 1 if b.desc.dxb else 0
             self.conv_mode = mode
             return
         if mode not in CONV_MODES:
@@ -357,7 +357,7 @@ class FlowEngine:
                 b.desc.wx3 = on if b.wx3_u else 0
                 b.desc.dx3 = 1 if (dl and b.dx3_w and b.desc.wx3) else 0
                 # round 5's dx3 fuses the heads; dx3w16 (round 4's arithmetic) keeps the GEMMs
-                b.desc.fuse_head = 1 if (mode == "dx3" and b.desc.dx3 and HEAD_FUSE) else 0
+                b.desc.fuse_head = 1 if (mode == "dx3" and b.desc.dx3) else 0
         self.conv_mode = mode  # each mode's top prior is cached separately (_top_prior)
 
     @property
@@ -459,6 +459,13 @@ class FlowEngine:
                     extra = max(extra, int(w))
             # + the fused head's running sums [P][16] (and the split-K workspace)
             n = max(n, P * self.ld_tmp + (extra + 512) // 4 + 32 * P)
+            # at least what the library lays out for each block as currently set up (the split
+            # copy, split-K workspace and head sums: idf_dense_block_dx3_tmp_bytes)
+            for b in self.couple[l] + [self.prior[l]]:
+                nb = int(lib().idf_dense_block_dx3_tmp_bytes(ctypes.byref(b.desc), B, Lv.h, Lv.w))
+                if nb < 0:
+                    raise IdfError(f"dense block tmp size query failed at level {l}")
+                n = max(n, (nb + 255) // 4)
         return n
 
     def tmp_pitch(self, ws, P: int) -> int:

@@ -204,7 +204,8 @@ typedef struct IdfDenseBlock {
   int32_t dx3;
   float dx3_yscale[IDF_MAX_DEPTH];
   const uint16_t *dx3_w[IDF_MAX_DEPTH];
-  /* fuse_head = 1: when every layer runs on dx3 (with one output group) and n_head <= 16, the
+  /* fuse_head = 1: when every layer runs on dx3 (with one output group), n_head <= 16 and
+   * k_in[0] <= 64 (the geometry alone decides; idf_dense_block_dx3_tmp_bytes), the
    * 1x1 head (nnblock.py:48-51) is not a separate GEMM over the whole feature buffer: its sums
    * start from the block input (idf_dx3_head_init) and every dx3 layer's epilogue adds its own
    * outputs' share (IdfDx3Head); the last layer applies the head epilogue.  keep_feat = 0 then
@@ -236,14 +237,23 @@ typedef struct IdfHeadOut {
 /* Run a whole DenseBlock over B images of HxW.  `feat` (pixel-major, row stride
  * ld_feat >= k_in[depth] rounded to 16) must hold the block input in columns
  * [0, k_in[0]) (zero-padded); columns beyond are overwritten.  `tmp` is a
- * scratch [P][ld_tmp] buffer for the 1x1 outputs.  The head GEMM runs with the
- * epilogue `head` describes; head == NULL skips the head (the caller runs it with
- * idf_conv1x1_f32).
+ * scratch [P][ld_tmp] buffer (256-B aligned) for the 1x1 outputs, the Winograd / halo
+ * workspaces and -- for a block on the direct convs (dx3 / dxb) -- at least
+ * idf_dense_block_dx3_tmp_bytes(blk, B, H, W) bytes: the split (or bf16) feature copy,
+ * then the layers' split-K workspace (256-B aligned), then with a fused head its running
+ * sums, P * 64 bytes (256-B aligned).  A smaller tmp is IDF_ERR_WORKSPACE -- never a quiet
+ * switch to the head GEMM, whose sums run in another order (the fusion is part of the
+ * conv arithmetic a bitstream's conv code names).  The head runs with the epilogue `head`
+ * describes; head == NULL skips the head (the caller runs it with idf_conv1x1_f32).
  * Replaces DenseBlock.forward (nnblock.py:53-56) + the Round/add of
  * AdditiveCouple (couplelib.py:47-61) or the split of Prior (priorlib.py:36-47). */
 int idf_dense_block_f32(void *stream, const IdfDenseBlock *blk, int32_t B, int32_t H, int32_t W,
                         float *d_feat, int64_t ld_feat, float *d_tmp, int64_t ld_tmp,
                         const IdfHeadOut *head);
+/* Bytes of tmp the block's direct-conv layers and fused head need at B images of HxW (0: the
+ * block runs no dx3 / dxb layer there; -1: bad arguments).  A function of the block and the
+ * geometry only. */
+int64_t idf_dense_block_dx3_tmp_bytes(const IdfDenseBlock *blk, int32_t B, int32_t H, int32_t W);
 
 /* Live kernel timing with HIP events (bench.py's roofline): a timer records an
  * event pair around every GEMM launch of the dense blocks run through

@@ -160,3 +160,18 @@ def test_range_guard_clean_on_real_batch():
     eng.clear_range_flag()
     bs = codec.encode(synthetic.images(64, seed=5).cuda())
     assert bs.meta["conv"] == "dx3" and not eng.range_flag_tripped()
+
+
+def test_round4_code6_bitstream_decodes_exactly(golden):
+    """A conv-code-6 bitstream written by the round-4 build itself (tests/golden/
+    imagenet64_code6_r4.npz, from make_code6_fixture.py at 23b932c: round 4's dx3 at the 16-wide
+    levels) decodes with today's library to the exact images: code 6 ("dx3w16") still names the
+    arithmetic it was written with, bit for bit."""
+    from idfcodec.codec import Bitstream
+    d = golden("imagenet64_code6_r4.npz")
+    bs = Bitstream.from_bytes(d["bitstream"].tobytes())
+    assert bs.meta["conv"] == "dx3w16"
+    model = _imagenet64()
+    out, info = model.codec().decode(bs)
+    assert info["ok"], info
+    assert torch.equal(out.cpu(), torch.from_numpy(d["images"])), "round-4 file decodes wrong"

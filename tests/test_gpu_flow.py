@@ -153,17 +153,16 @@ def test_model_vs_oracle_teacher_forced_levels(golden, name):
 
 
 # Round flips against a CPU fp32 run of the same model and images.  A flip cascades through
-# the later couplings and levels, and any fp32 reassociation starts one: tools/flip_probe.py
-# (profiles/r05/flips/flip_probe.log) measured, per level, vs the reference's recorded B=2
-# latents: dx3 [3, 18, 150], exact-f32 Winograd [1, 16, 126] of [12288, 6144, 6144] (the
-# oracle itself [0, 0, 0]: it is the reference, bit for bit); vs the oracle at B=16: dx3
-# [5, 39, 379], f32 [2, 25, 294] of [98304, 49152, 49152] -- the folded 1x1 alone sets the
-# cascade, the split-f16 products add little.  The bounds are twice the dx3 counts.
-FLIP_BOUND_REF_B2 = (6, 36, 300)
-FLIP_BOUND_ORACLE_B16 = (10, 78, 758)
-# per coupling, teacher-forced (no cascade): measured (dx3, B=16) 6 / 393216, 2 / 196608,
-# 1 / 98304 flips per level, <= 1.6e-5 of the rounded values; bound 5e-5 (3x)
-COUPLE_FLIP_BOUND = 5e-5
+# the later couplings and levels, and any fp32 reassociation starts one.  Measured with the fused
+# DenseBlock head (round 5, profiles/r05/fused_head/parity.log), per level of [12288, 6144, 6144]
+# latents vs the reference's recorded B=2 run: [0, 0, 0]; of [98304, 49152, 49152] vs the oracle at
+# B=16: [0, 0, 8]; per coupling, teacher-forced (no cascade): [0, 0, 1] of [393216, 196608,
+# 98304].  (Before the fused head: [3, 18, 150], [5, 39, 379], [6, 2, 1].)  Each bound is
+# max(2x the measured count, 4), so a summation-order change that moves roundings -- the paired
+# split schedule gave [0, 4, 50] vs the reference (profiles/r05/pairs/) -- fails here.
+FLIP_BOUND_REF_B2 = (4, 4, 4)
+FLIP_BOUND_ORACLE_B16 = (4, 4, 16)
+COUPLE_FLIP_BOUND = (4, 4, 4)
 
 
 def test_imagenet64_forward_vs_oracle_b16():
@@ -183,7 +182,8 @@ def test_imagenet64_forward_vs_oracle_b16():
     rl, _, _ = o.forward(x)
     flips = [int((a.cpu() != b).sum()) for a, b in zip(lat, rl)]
     sizes = [b.numel() for b in rl]
-    print(f"flips vs the fp32 oracle per level (B=16, dx3): {flips} of {sizes}")
+    print(f"flips vs the fp32 oracle per level (B=16, dx3): {flips} of {sizes}; "
+          f"bounds {FLIP_BOUND_ORACLE_B16}")
     for i in range(3):
         assert flips[i] <= FLIP_BOUND_ORACLE_B16[i], (i, flips[i], sizes[i])
     assert torch.equal(model.generated_from_latents(lat), x.cuda())
@@ -220,9 +220,10 @@ def test_imagenet64_coupling_flips_teacher_forced():
             per_level.append((fl, tot))
             if lvl < o.nsplit - 1:
                 x = x[:, x.shape[1] // 2:]
-    print(f"coupling Round flips per level, teacher-forced (B=16, dx3): {per_level}")
-    for fl, tot in per_level:
-        assert fl <= COUPLE_FLIP_BOUND * tot, (fl, tot)
+    print(f"coupling Round flips per level, teacher-forced (B=16, dx3): {per_level}; "
+          f"bounds {COUPLE_FLIP_BOUND}")
+    for i, (fl, tot) in enumerate(per_level):
+        assert fl <= COUPLE_FLIP_BOUND[i], (i, fl, tot)
 
 
 def test_imagenet64_forward_vs_reference(golden):
@@ -239,10 +240,10 @@ def test_imagenet64_forward_vs_reference(golden):
     # a flipped Round cascades through later couplings (fp32 vs fp64
     # already flips 0.46% at the top level), so only the rate is bounded here --
     # the 1e-5 parity is asserted teacher-forced in test_imagenet64_x3_blocks_teacher_forced.
-    # Bound: FLIP_BOUND_REF_B2, twice the measured counts (printed)
+    # Bound: FLIP_BOUND_REF_B2, max(2x the measured counts, 4) (printed)
     flips = [int((lat[i].cpu() != torch.from_numpy(d[f"latent{i}"])).sum()) for i in range(3)]
     sizes = [int(d[f"latent{i}"].size) for i in range(3)]
-    print(f"flips vs the reference per level: {flips} of {sizes}")
+    print(f"flips vs the reference per level: {flips} of {sizes}; bounds {FLIP_BOUND_REF_B2}")
     for i in range(3):
         assert flips[i] <= FLIP_BOUND_REF_B2[i], (i, flips[i], sizes[i])
     assert torch.equal(model.generated_from_latents(lat), x)

@@ -34,6 +34,40 @@ def test_library_exports_every_declared_symbol():
     assert lib.idf_version().decode().startswith("idfcodec")
 
 
+def test_fused_head_tmp_is_required_not_optional():
+    """A dx3 block whose head fuses (by its geometry alone) needs idf_dense_block_dx3_tmp_bytes of
+    tmp: one byte less is IDF_ERR_WORKSPACE (no quiet switch to the head GEMM, whose sums run in
+    another order), and the need does not depend on the room offered.  Host-side checks only:
+    the call returns before any launch."""
+    import ctypes
+    from idfcodec import _lib
+    lib = _lib.lib()
+    d = _lib.IdfDenseBlock()
+    d.depth, d.g_pad, d.n_head, d.fold, d.wx3, d.dx3, d.fuse_head = 2, 44, 12, 1, 1, 1, 1
+    for i, c in enumerate((12, 56, 100)):
+        d.k_in[i] = c
+    for i in range(2):
+        d.dx3_w[i] = 0x100000 * (i + 1)  # never dereferenced before the workspace check
+    B, H, W = 4, 8, 8  # the split-K level: its partial sums make the need exceed P * k_in[2] * 4
+    P = B * H * W
+    need = int(lib.idf_dense_block_dx3_tmp_bytes(ctypes.byref(d), B, H, W))
+    assert need >= P * (4 * 64 + 64)  # at least the split copy (4 slabs) and the head sums
+    d.fuse_head = 0
+    need_nf = int(lib.idf_dense_block_dx3_tmp_bytes(ctypes.byref(d), B, H, W))
+    assert need - need_nf >= P * 64
+    d.fuse_head = 1
+    head = _lib.IdfHeadOut()
+    head.mode = _lib.EPI_STORE
+    ld_tmp = (need - 1) // (4 * P)  # floats per pixel: P * ld_tmp * 4 < need
+    assert P * ld_tmp * 4 < need and ld_tmp >= 100 and (need - P * 64) < P * ld_tmp * 4
+    fake = ctypes.c_void_p(0x7f0000000000)  # 256-B aligned, never touched
+    rc = lib.idf_dense_block_f32(None, ctypes.byref(d), B, H, W, fake, 112, fake, ld_tmp,
+                                 ctypes.byref(head))
+    assert rc == 3, _lib.ERR_NAMES.get(rc, rc)  # IDF_ERR_WORKSPACE
+    d.n_head = 17  # no fusion for heads of > 16 outputs: only the copy and split-K part
+    assert int(lib.idf_dense_block_dx3_tmp_bytes(ctypes.byref(d), B, H, W)) == need_nf
+
+
 def test_struct_layout_matches_header():
     """ctypes mirror of IdfDenseBlock / IdfHeadOut == the C layout (compiled probe)."""
     from idfcodec import _lib
@@ -447,3 +481,13 @@ def test_decode_rejects_mismatched_container():
     bad[6] = 0x3F  # unknown conv code in the flags
     with pytest.raises(ValueError):
         Bitstream.from_bytes(bytes(bad))
+
+
+def test_round4_code6_fixture_header(golden):
+    """The round-4 fixture (tests/golden/make_code6_fixture.py at 23b932c) is a version-2 container
+    with conv code 6, which reads as "dx3w16"; its decode is tests/test_gpu_codec.py's."""
+    from idfcodec.codec import Bitstream
+    d = golden("imagenet64_code6_r4.npz")
+    bs = Bitstream.from_bytes(d["bitstream"].tobytes())
+    assert bs.meta["conv"] == "dx3w16" and bs.n_images == d["images"].shape[0] == 4
+    assert bs.to_bytes() == d["bitstream"].tobytes()  # re-serialises byte for byte
