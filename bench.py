@@ -285,6 +285,42 @@ def _cpu_chunk(o, img):
     return t_enc, t_dec, bool(torch.equal(xd, x))
 
 
+def bpp_vs_oracle(model_cfg, img_u8, bs, B, n=16):
+    """BASELINE's "bpp vs reference": the first n images of this rank's batch coded by the
+    oracle (the torch-fp32 flow pinned bit for bit to the reference's modules + the C rANS
+    pinned to the reference's rans.cpp) and by the device, in the reference's accounting
+    (trainer.py:326-327: 64 bits per stream's final state + 32 per word, over the sub-pixels).
+    The device side counts the same images' streams of the timed steps' last bitstream (level-
+    major, image-minor: stream (l, b) = l * B + b).  Any difference comes from Round flips of
+    the fp32 flows (tests/test_gpu_flow.py bounds them)."""
+    import numpy as np
+    o = _cpu_oracle(model_cfg)  # (puts oracle/ on the path)
+    import flow_oracle as FO
+    import rans_oracle as RO
+    x = FO.dequant(img_u8[:n].cpu())
+    lat, me, ls = o.forward(x)
+    flat = lambda ts: np.concatenate([t.reshape(-1).numpy() for t in ts])  # noqa: E731
+    sizes = [t[0].numel() for t in lat]
+    off = [0]
+    for m in sizes:
+        off += [off[-1] + m * (b + 1) for b in range(n)]
+    _, _, nw, st = RO.encode_streams(np.asarray(off, np.int64), flat(lat), flat(me),
+                                     flat([torch.exp(t) for t in ls]))
+    nsub = n * 3 * PX_PER_IMG
+    bits_o = 64 * len(nw) + 32 * int(np.asarray(nw, np.int64).sum())
+    hn = bs.nwords_host()
+    k = [lv * B + b for lv in range(len(sizes)) for b in range(n)]
+    bits_g = 64 * len(k) + 32 * int(hn[k].sum())
+    return {"images": n, "bpp_oracle": round(3.0 * bits_o / nsub, 5),
+            "bpp_device": round(3.0 * bits_g / nsub, 5),
+            "bpp_difference": round(3.0 * (bits_g - bits_o) / nsub, 6),
+            "bits_oracle": bits_o, "bits_device": bits_g,
+            "oracle_status_ok": bool((np.asarray(st) == 0).all()),
+            "oracle": ("oracle/flow_oracle.py (torch fp32, pinned to the reference modules) + "
+                       "oracle/rans_oracle.c (pinned to the reference's rans.cpp), on the "
+                       "bench's own first images")}
+
+
 def _cpu_run(o, img, chunk):
     te = td = 0.0
     ok = True
@@ -507,15 +543,16 @@ def roofline_pass(codec, eng, timer, img):
 
 
 def residual_extras(args):
-    """BASELINE configs[2..4] (the residual VQ-VAE + flow codecs): one short run each on this
-    rank's GPU (sharded per rank when N > 1, bitstreams gathered to rank 0 in the timed
-    encode), reported beside the headline."""
+    """BASELINE configs[2..4] (the residual VQ-VAE + flow codecs): 10 timed steps after 2
+    warm-up each on this rank's GPU (sharded per rank when N > 1, bitstreams gathered to rank 0
+    in the timed encode), with the flow convs' and the VQ-VAE kernels' rooflines and the
+    encode / decode phase split, reported beside the headline."""
     sys.path.insert(0, os.path.join(REPO, "tools"))
     import bench_residual
     out = {}
     for name in ("resflow-cond-imagenet64", "resflows_smallpatch_split", "resflow-patches-vqvae"):
         try:
-            r = bench_residual.run(name, steps=2, warmup=1)
+            r = bench_residual.run(name, steps=10, warmup=2)
         except Exception as e:  # reported, never hides the headline
             r = {"error": repr(e)}
             if dist.is_initialized():
@@ -525,7 +562,9 @@ def residual_extras(args):
                                            "decode_ms", "batch_per_gpu", "image", "bpp",
                                            "round_trip_exact", "dtype", "n_gpus",
                                            "vq_indices_ms", "vq_reconstruct_ms", "vq_conv",
-                                           "roofline") if k in r} \
+                                           "roofline", "vq_roofline", "encode_split_ms",
+                                           "decode_split_ms", "steps", "warmup",
+                                           "round_trip_exact_steps") if k in r} \
                 if "error" not in r else r
     return out
 
@@ -710,6 +749,12 @@ def main():
         del whole, img_full
     bits = full.bits() if full is not None else bs.bits()
     bpp = 3.0 * bits / (3 * B * world * PX_PER_IMG)
+    bpp_ref = None
+    if rank == 0 and not args.no_cpu_baseline:
+        try:
+            bpp_ref = bpp_vs_oracle(cfg, img, bs, B)
+        except Exception as e:  # reported, never hides the headline
+            bpp_ref = {"error": repr(e)}
 
     timer = _lib.lib().idf_timer_create(8192)
     c3_tflops, c3_avg_ms, c3_n, c3_flops = roofline_pass(codec, eng, timer, img)
@@ -796,6 +841,7 @@ def main():
             "serial": serial,
             "bpp": round(bpp, 4),
             "bits_per_subpixel": round(bpp / 3, 4),
+            "bpp_vs_reference": bpp_ref,
             "round_trip_exact": exact and n_exact == n_checked,
             "round_trip_exact_steps": f"{n_exact}/{n_checked}",
             "round_trip_check": ("every timed step's decoded batch compared with its input on "

@@ -112,6 +112,15 @@ class ResidualCodec:
         self.conditional = type(flows_model).__name__ == "ConditionalFlows"
         self.bits = max(1, math.ceil(math.log2(vqvae.embed_num)))
         self.pad = (int(pad[0]), int(pad[1]))
+        # bench timing (tools/bench_residual.py): when a list, encode / decode append
+        # (phase name, HIP event) at each phase's end on the current stream
+        self.phases = None
+
+    def _mark(self, name):
+        if self.phases is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self.phases.append((name, e))
 
     @staticmethod
     def _edge(img_u8, Ho, Wo):
@@ -158,24 +167,32 @@ class ResidualCodec:
             raise ValueError(f"image size {src_hw}: the codec takes {(self.H, self.W)}"
                              + (f" or {(self.H - self.pad[0], self.W - self.pad[1])}"
                                 if any(self.pad) else ""))
+        self._mark("start")
         data = self._dequant(img_u8)
+        self._mark("pad_dequant")
         idx = self.vqvae.indices(data)                       # [B, h, w] int32
+        self._mark("vq_indices")
         rec = self.vqvae.reconstruct(idx)                    # NCHW on the grid
+        self._mark("vq_reconstruct")
         vq_conv = self.vqvae.engine().last_decode_mode       # what the receiver must run
         res = self._pointwise(2, data, rec)                  # data - rec
         res_p, _ = self.patch.forward(res, None)
         codec = self._codec()
         if self.conditional:
             rec_p, _ = self.patch.forward(rec, None)
+            self._mark("residual_patching")
             flow = codec.encode_nchw(res_p, cond=rec_p.contiguous())
         else:
+            self._mark("residual_patching")
             flow = codec.encode_nchw(res_p)
+        self._mark("flow_encode")
         per = idx.shape[1] * idx.shape[2]
         nwd = int(lib().idf_pack_bits_words(B, per, self.bits))
         words = torch.empty(max(nwd, 1), dtype=torch.int32, device=img_u8.device)
         check(lib().idf_pack_bits(_lib.stream_ptr(img_u8.device), B, per, self.bits, ptr(idx),
                                   ptr(words)), "pack idx")
         words = words[:nwd]
+        self._mark("index_code")
         return ResidualBitstream(flow, words, B, (C, H, W), tuple(idx.shape[1:]),
                                  self.vqvae.embed_num, None if src_hw == (H, W) else src_hw,
                                  vq_conv)
@@ -191,15 +208,21 @@ class ResidualCodec:
         if words.numel() == 0:
             words = torch.zeros(1, dtype=torch.int32, device=dev)
         idx = torch.empty(n, dtype=torch.int32, device=dev)
+        self._mark("start")
         check(lib().idf_unpack_bits(_lib.stream_ptr(dev), B, h * w, self.bits, ptr(words),
                                     ptr(idx)), "unpack idx")
+        self._mark("index_code")
         rec = self.vqvae.reconstruct(idx.view(B, h, w), conv=rbs.vq_conv)
+        self._mark("vq_reconstruct")
         codec = self._codec()
         if self.conditional:
             rec_p, _ = self.patch.forward(rec, None)
+            self._mark("patching")
             res_p, info = codec.decode_nchw(rbs.flow, cond=rec_p.contiguous(), verify=verify)
         else:
+            self._mark("patching")
             res_p, info = codec.decode_nchw(rbs.flow, verify=verify)
+        self._mark("flow_decode")
         res = self.patch.backward(res_p.contiguous())
         data = self._pointwise(3, res, rec)                  # res + rec
         s = _lib.stream_ptr(dev)
@@ -210,6 +233,7 @@ class ResidualCodec:
         check(lib().idf_quant_u8(s, B, C, H, W, ptr(pm), 4, ptr(img), ptr(bad)), "quant")
         if rbs.source_hw:
             img = self._edge(img, *rbs.source_hw)
+        self._mark("unpatch_quant_crop")
         info["off_grid"] = bad
         if verify:
             info["ok"] = bool(info.get("ok", True)) and int(bad.item()) == 0

@@ -218,6 +218,9 @@ class VQEngine:
         if self.conv_mode not in VQ_CONV_MODES:
             raise ValueError(f"IDF_VQ_CONV={self.conv_mode!r}: one of {VQ_CONV_MODES}")
         self.last_decode_mode = self.conv_mode
+        # bench timing (tools/bench_residual.py vq_roofline): when a list, every conv and argmin
+        # launch appends (kind, algorithmic FLOPs, event before, event after) on its stream
+        self.timer = None
         self.flag = torch.zeros(1, dtype=torch.int32, device=device)
         self._mode = self.conv_mode  # the mode of the pass being run
         self._ws = None
@@ -235,8 +238,34 @@ class VQEngine:
         return (st, [DevConv(c, self.device, self.wino) for c in st.convs])
 
     # ---------------------------------------------------------------- conv runner
+    def _timed(self, kind, flops):
+        """(start, finish) callables around one launch: HIP events on the current stream when
+        self.timer is a list, no-ops otherwise."""
+        if self.timer is None:
+            return lambda: None, lambda: None
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        self.timer.append((kind, float(flops), a, b))
+        return a.record, b.record
+
     def _conv(self, s, dc: DevConv, x, B, H, W, ldx, act, out, ldo, Ho, Wo, res=None, ldr=0,
               check_in=1):
+        c = dc.c
+        if self.timer is not None:
+            # algorithmic FLOPs: 2 x taps x cin x cout per computed output (the Winograd 3x3
+            # priced as the direct conv it computes; a transposed conv's launch covers one output
+            # parity: its taps on the input grid)
+            grid = B * (H * W if (dc.wino_u is not None or c.osy == 2) else Ho * Wo)
+            kind = ("resblock3x3_" + self._mode) if dc.wino_u is not None else "conv_taps"
+            t0, t1 = self._timed(kind, 2.0 * grid * len(c.dy) * c.cin * c.cout)
+        else:
+            t0 = t1 = lambda: None
+        t0()
+        self._conv_launch(s, dc, x, B, H, W, ldx, act, out, ldo, Ho, Wo, res, ldr, check_in)
+        t1()
+
+    def _conv_launch(self, s, dc: DevConv, x, B, H, W, ldx, act, out, ldo, Ho, Wo, res, ldr,
+                     check_in):
         c = dc.c
         if dc.wino_u is not None:
             L = lib()
@@ -333,9 +362,12 @@ class VQEngine:
         idx = torch.empty(B * h * w, dtype=torch.int32, device=self.device)
         nws = int(lib().idf_vq_argmin_workspace_bytes(B * h * w, self.K))
         ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=self.device)
+        t0, t1 = self._timed("argmin", 2.0 * B * h * w * self.D * self.K)
+        t0()
         check(lib().idf_vq_argmin_ws(s, B * h * w, self.D, ptr(z), round_up(self.D, 4),
                                      ptr(self.embed), self.D, self.K, ptr(self.enorm), ptr(idx),
                                      ptr(ws), nws), "vq argmin")
+        t1()
         return idx, (h, w), z
 
     def decode_pm(self, idx, B, h, w, mode=None):

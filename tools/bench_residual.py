@@ -93,7 +93,60 @@ def flow_conv_roofline(codec, fl, img):
             "frac": round(achieved / peak, 4), "conv_mode": mode}
 
 
-def run(config: str, batch: int | None = None, steps: int = 2, warmup: int = 1,
+VQ_PEAK = {"conv_taps": ("f32 MFMA", 157.3), "argmin": ("f32 MFMA", 157.3),
+           "resblock3x3_x3": ("f16 MFMA (split-f16 products)", 2500.0),
+           "resblock3x3_f32": ("f32 MFMA", 157.3)}
+VQ_KERNEL = {"conv_taps": "conv_taps_kernel (strided / transposed VQ-VAE convs as tap GEMMs)",
+             "argmin": "vq_argmin_kernel (+vq_argmin_merge_kernel): fused distance + running "
+                       "min over the codebook, 2*D*K FLOP per latent",
+             "resblock3x3_x3": "conv3_wino_kernel<..., true, ...> via idf_conv3x3_wx3_res "
+                               "(ResBlock 3x3, split-f16 Winograd, residual fused)",
+             "resblock3x3_f32": "conv3_wino_kernel via idf_conv3x3_wino_res (exact f32)"}
+
+
+def vq_roofline(codec, img):
+    """The VQ-VAE's kernels timed live over one encode + decode after the timed steps: HIP
+    events around every conv and argmin launch on its stream (VQEngine.timer).  Per kind:
+    launches, milliseconds per encode + decode, algorithmic FLOPs (2 x taps x cin x cout per
+    computed output; the Winograd ResBlock convs priced as the direct 3x3 they compute; argmin
+    2 x D x K per latent) over the summed launch time, against the dense peak of the kind's
+    arithmetic."""
+    vqe = codec.vqvae.engine()
+    vqe.timer = []
+    try:
+        codec.decode(codec.encode(img), verify=False)
+        torch.cuda.synchronize()
+        recs = vqe.timer
+    finally:
+        vqe.timer = None
+    out = {}
+    for kind in sorted({r[0] for r in recs}):
+        rs = [r for r in recs if r[0] == kind]
+        ms = sum(a.elapsed_time(b) for _, _, a, b in rs)
+        fl = sum(r[1] for r in rs)
+        what, peak = VQ_PEAK[kind]
+        tf = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+        out[kind] = {"kernel": VQ_KERNEL[kind], "launches": len(rs), "ms": round(ms, 3),
+                     "gflop": round(fl / 1e9, 3), "achieved": round(tf, 3), "peak": peak,
+                     "peak_of": what, "unit": "TFLOP/s", "frac": round(tf / peak, 4)}
+    tot = sum(v["ms"] for v in out.values())
+    dom = max(out, key=lambda k: out[k]["ms"]) if out else None
+    return {"per_kind": out, "vq_kernel_ms_per_encode_decode": round(tot, 3),
+            "dominant": dom, "bound": "mfma",
+            "sampled": "every VQ-VAE conv / argmin launch of one encode + decode after the "
+                       "timed steps"}
+
+
+def phase_split(phases, steps):
+    """Mean ms per phase of the timed steps from ResidualCodec's (name, event) marks."""
+    acc = {}
+    for marks in phases:
+        for (_, a), (name, b) in zip(marks, marks[1:]):
+            acc[name] = acc.get(name, 0.0) + a.elapsed_time(b)
+    return {k: round(v / steps, 3) for k, v in acc.items()}
+
+
+def run(config: str, batch: int | None = None, steps: int = 10, warmup: int = 2,
         precision: str | None = None) -> dict | None:
     """One residual config's encode+decode throughput on this rank's GPU (the process group,
     if any, already initialised).  Returns the result dict on rank 0, None elsewhere."""
@@ -130,22 +183,32 @@ def run(config: str, batch: int | None = None, steps: int = 2, warmup: int = 1,
     sync()
     te = td = 0.0
     merged = None
+    enc_marks, dec_marks = [], []
+    n_exact = 0
     for _ in range(steps):
         sync()
         t0 = time.perf_counter()
+        codec.phases = []
         rbs = codec.encode(img)
         if world > 1:
             merged = gather_residual(rbs)
         torch.cuda.synchronize()
+        enc_marks.append(codec.phases)
         t1 = time.perf_counter()
+        codec.phases = []
         out, info = codec.decode(rbs, verify=False)
         torch.cuda.synchronize()
+        dec_marks.append(codec.phases)
+        codec.phases = None
         t2 = time.perf_counter()
         te += t1 - t0
         td += t2 - t1
-    exact = bool(torch.equal(out, img))
+        n_exact += int(torch.equal(out, img))  # every timed step's round trip (after its timing)
+    exact = n_exact == steps
     t_idx, t_rec = vq_time()
     roof = flow_conv_roofline(codec, fl, img)
+    vroof = vq_roofline(codec, img)
+    enc_split, dec_split = phase_split(enc_marks, steps), phase_split(dec_marks, steps)
     if world > 1:
         t = torch.tensor([te, td, t_idx, t_rec, 0.0 if exact else 1.0], device=dev)
         all_reduce(t, dist.ReduceOp.MAX)
@@ -159,7 +222,8 @@ def run(config: str, batch: int | None = None, steps: int = 2, warmup: int = 1,
             "metric": f"encode+decode Mpixels/s ({config}, bit-exact round trip)",
             "value": round(px * steps / (te + td) / 1e6, 4), "unit": "Mpx/s", "n_gpus": world,
             "batch_per_gpu": per, "image": [3, Hs, Ws], "coded_image": [3, H, W],
-            "steps": steps, "encode_ms": round(te / steps * 1e3, 2),
+            "steps": steps, "warmup": warmup, "round_trip_exact_steps": f"{n_exact}/{steps}",
+            "encode_ms": round(te / steps * 1e3, 2),
             "decode_ms": round(td / steps * 1e3, 2),
             "encode_mpx_s": round(px * steps / te / 1e6, 4),
             "decode_mpx_s": round(px * steps / td / 1e6, 4),
@@ -167,7 +231,12 @@ def run(config: str, batch: int | None = None, steps: int = 2, warmup: int = 1,
             "bpp": round(3 * bs.bpd(), 4), "index_bits_share": round(
                 1 - bs.flow.bits() / bs.bits(), 4),
             "round_trip_exact": exact, "scaling": "weak",
-            "vq_conv": rbs.vq_conv, "roofline": roof,
+            "vq_conv": rbs.vq_conv, "roofline": roof, "vq_roofline": vroof,
+            "encode_split_ms": enc_split, "decode_split_ms": dec_split,
+            "split_note": ("device time between phase marks on the codec's stream, mean over "
+                           "the timed steps (the flow phase includes its side-stream rANS "
+                           "joins; host-side waits such as the VQ range-guard read sit in the "
+                           "phase that issues them)"),
             "dtype": ("bf16 flow convs (f32 accumulate), f32 heads/VQ-VAE/CDF"
                       if fl.engine().precision == "bf16" else "f32"),
             "data": "synthetic uint8, seeded weights"}
@@ -180,8 +249,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="resflow-cond-imagenet64")
     ap.add_argument("--batch", type=int, default=None, help="images per GPU")
-    ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--precision", default=None, choices=[None, "f32", "bf16"])
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
