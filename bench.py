@@ -187,7 +187,10 @@ def conv_kernel_name(eng):
                 "split-f16 products over the block's split feature copy (x = xh + xl written once "
                 "by the producer, halos by LDS-DMA; xh.wh + xl.wh + xh.wl on "
                 "v_mfma_f32_16x16x32_f16, f32 accumulation), the DenseBlock head's share added in "
-                "the epilogue")
+                "the epilogue; the 16x16 and 8x8 levels' DenseBlocks each as ONE launch "
+                "(conv3_dx3_block_kernel<3, ...>: a workgroup per tile looping over the 12 "
+                "layers, the 8x8 split-K chunks summed in the block, the head's sums in "
+                "registers) -- bit for bit the per-layer launches")
     if eng.wino and eng.conv_mode == "x3":
         return ("conv3_wino_kernel<3, 448, true, false> (+conv3_wino_reduce_kernel at 8x8): "
                 "DenseLayer 3x3 conv with the 1x1 folded in, Winograd F(2x2,3x3), split-f16 "
@@ -493,20 +496,25 @@ def cpu_baseline(model_cfg, n_img, runs, chunk=16):
 
 def conv_algorithmic_bytes(eng, B):
     """(launches, algorithmic HBM bytes) of one encode's DenseLayer convs -- the launches
-    roofline_pass times: per launch the layer's c input channels read and g outputs written,
-    fp32, per pixel, plus its Winograd weights (16 positions x c x g f16 hi/lo pairs, 4 B)."""
+    roofline_pass times: per layer the c input channels read and g outputs written, fp32, per
+    pixel, plus its weights (9 direct taps or 16 Winograd positions x c x g f16 hi/lo pairs,
+    4 B); a fused DenseBlock (engine.fused_block: every layer in one launch) is one launch
+    carrying its layers' bytes."""
     n = byt = 0
     for l, L in enumerate(eng.levels):
         P = B * L.h * L.w
         # IDFlows' top prior sees zeros: computed once per model, not per encode
         cached = L.prior_x_zero and not eng.conditional
-        for geom in [b.geom for b in eng.couple[l]] + ([] if cached else [eng.prior[l].geom]):
+        for blk in list(eng.couple[l]) + ([] if cached else [eng.prior[l]]):
+            geom = blk.geom
             c = geom.a
             nd = eng.dx3_layers(l, geom)
+            fused = eng.fused_block(l, blk)
+            n += 1 if fused else 0
             for i, g in enumerate(geom.growth):
                 # weights per (c, g): 16 Winograd positions or 9 direct taps, f16 (hi, lo) pairs
                 npos = 9 if i < nd else 16
-                n += 1
+                n += 0 if fused else 1
                 byt += 4 * P * (c + g) + npos * c * g * 4
                 c += g
     return n, byt
@@ -762,7 +770,8 @@ def main():
 
     flops = eng.flops_per_image()["total"]
     # both range-check variants of the kernels: roofline_pass times every DenseLayer conv launch
-    knames = {"dx3": ("conv3_dx3_kernel<3,", "conv3_wino_kernel<3, 448, true,"),
+    knames = {"dx3": ("conv3_dx3_kernel<3,", "conv3_dx3_block_kernel<3,",
+                      "conv3_wino_kernel<3, 448, true,"),
               "x3": ("conv3_wino_kernel<3, 448, true,",),
               "f32": ("conv3_wino_kernel<3, 448, false",)}[eng.conv_mode] if eng.wino else ()
     traffic, traffic_src = pmc_traffic(knames, c3_n) if eng.wino else (None, None)
@@ -854,7 +863,8 @@ def main():
             "roofline": {
                 "kernel": kdesc,
                 "flops_per_launch": "2*P*9*c*g (P = B*h*w pixels, c/g unpadded in/out "
-                                    "channels of the layer)",
+                                    "channels of the layer; a fused DenseBlock launch sums "
+                                    "its layers)",
                 "algorithmic_gflop_per_launch": round(c3_flops / 1e9, 3),
                 "sampled": ("every DenseLayer conv launch (8 couplings + prior, every level) of "
                             "one encode after the timed steps, side-stream rANS encode off"),

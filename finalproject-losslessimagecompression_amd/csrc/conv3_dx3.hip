@@ -288,6 +288,32 @@ __device__ __forceinline__ DxTile dx_tile(const Dx3Args& g, int tile) {
   return t;
 }
 
+// One DenseLayer's own parameters (the rest of Dx3Args is the block's): a single-layer launch
+// takes them from Dx3Args, the fused DenseBlock kernel (conv3_dx3_block_kernel) from its layer
+// list.  nchunk / chunk_slabs: the layer's split-K cut (dx3_launch_shape; the fused kernel runs
+// only geometries without one).
+struct Dx3Layer {
+  const uint16_t* Wt;
+  const float *b3, *vtap, *bfull;
+  float* out;
+  float yscale;
+  int32_t C, nslab, nchunk, chunk_slabs, hlast;
+};
+
+// The fused DenseBlock (conv3_dx3_block_kernel): every layer of a block in one launch, one
+// workgroup per tile, for geometries whose tiles hold whole images (no halo crosses a tile:
+// dx3_self_contained), so a tile's layers depend only on its own earlier layers.  With a fused
+// head the running sums stay in registers from the head init (hx: the block input, fp32 rows of
+// hld_x floats, hc0 channels; hb: the head bias) to the last layer's epilogue.
+constexpr int kDxMaxLayers = 16;
+struct Dx3MLArgs {
+  Dx3Layer layer[kDxMaxLayers];
+  int32_t nlayers, hc0;
+  const float* hx;
+  int64_t hld_x;
+  const float* hb;
+};
+
 // The epilogue's two LDS tables: the bias table [16 border classes][NF * 16] (stage_bias's
 // values: b3 plus the in-image taps' share of the folded 1x1 bias) and the fused head's weights
 // on this layer's outputs [16][NF * 16] (zeros past nh and past N).  load() issues every global
@@ -301,33 +327,33 @@ struct Dx3Tables {
   float bt[11];     // thread n < NN: output n's b3, 9 tap biases and full bias (all 16 classes)
   float ht[HPER];   // head entries tid, tid + kDxThreads, ...
 
-  __device__ __forceinline__ void load(const Dx3Args& g, int grp, int tid) {
+  __device__ __forceinline__ void load(const Dx3Args& g, const Dx3Layer& Ly, int grp, int tid) {
     const int n = grp * NN + tid, nc = n < g.N ? n : 0;
     if (tid < NN) {
-      bt[0] = g.b3[nc];
-      if (g.vtap) {
+      bt[0] = Ly.b3[nc];
+      if (Ly.vtap) {
 #pragma unroll
-        for (int tap = 0; tap < 9; ++tap) bt[1 + tap] = g.vtap[tap * g.ldv + nc];
-        bt[10] = g.bfull[nc];
+        for (int tap = 0; tap < 9; ++tap) bt[1 + tap] = Ly.vtap[tap * g.ldv + nc];
+        bt[10] = Ly.bfull[nc];
       }
     }
     if (g.nh > 0) {
 #pragma unroll
       for (int i = 0; i < HPER; ++i) {
         const int e = tid + i * kDxThreads, o = e / NN, hn = grp * NN + e - o * NN;
-        if (e < NE) ht[i] = g.hw[(int64_t)(o < g.nh ? o : 0) * g.ldhw + g.C + (hn < g.N ? hn : 0)];
+        if (e < NE) ht[i] = g.hw[(int64_t)(o < g.nh ? o : 0) * g.ldhw + Ly.C + (hn < g.N ? hn : 0)];
       }
     }
   }
 
-  __device__ __forceinline__ void store(float* btab, float* htab, const Dx3Args& g, int grp,
-                                        int tid) const {
+  __device__ __forceinline__ void store(float* btab, float* htab, const Dx3Args& g,
+                                        const Dx3Layer& Ly, int grp, int tid) const {
     if (tid < NN) {
       const int n = grp * NN + tid;
 #pragma unroll
       for (int cls = 0; cls < 16; ++cls) {
         float v = bt[0];
-        if (g.vtap) {
+        if (Ly.vtap) {
 #pragma unroll
           for (int tap = 0; tap < 9; ++tap) {
             const int dy = tap / 3 - 1, dx = tap % 3 - 1;
@@ -350,8 +376,11 @@ struct Dx3Tables {
   }
 };
 
-template <int NF, int WR, int PITCH, int PLANE_KIB, bool BF>
-__global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
+// One launch's work: ML = false, one layer (conv3_dx3_kernel: a block = a chunk of the slabs of
+// one output group of T tiles); ML = true, every layer of a DenseBlock for one tile
+// (conv3_dx3_block_kernel, T = 1, one output group, no split K).
+template <int NF, int WR, int PITCH, int PLANE_KIB, bool BF, bool ML>
+__device__ __forceinline__ void dx3_block(const Dx3Args& g, const Dx3MLArgs* ml) {
   using L = Dx3Lds<NF, WR, PITCH, PLANE_KIB, BF>;
   constexpr int T = L::T, HR = L::HR, NS = L::NS;
   static_assert(L::WST % 1024 == 0, "weight stage must be whole 1-KiB DMA pieces");
@@ -371,12 +400,38 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   const int rem = bid - chunk * per_chunk;
   const int grp = udiv_s(rem, g.nblk_tiles);
   const int tb = rem - grp * g.nblk_tiles;
-  const int s0 = chunk * g.chunk_slabs;
-  const int s1 = min(g.nslab, s0 + g.chunk_slabs);
   // the wave's tile and first output row
   const int tw = wave / (kDxWaves / T);
   const int r0 = WR * (wave % (kDxWaves / T));
-  const int tile = tb * T + tw;
+  d4 hreg[WR];  // ML: the fused head's running sums, registers across the layers
+  const int nlayers = ML ? ml->nlayers : 1;
+  for (int li = 0; li < nlayers; ++li) {
+  // (ML) the block's indices passed through an opaque asm: everything derived from them below
+  // (DMA plan, canvas position, fragment offsets) is recomputed in every layer -- held across
+  // the layer loop it doubled the kernel's VGPRs and spilled
+  int tid_o = tid, lane_o = lane, wave_o = wave, tb_o = tb, tw_o = tw, r0_o = r0, grp_o = grp,
+      chunk_o = chunk;
+  if constexpr (ML) {
+    asm volatile("" : "+v"(tid_o), "+v"(lane_o), "+v"(wave_o), "+v"(tb_o), "+v"(tw_o), "+v"(r0_o),
+                 "+v"(grp_o), "+v"(chunk_o));
+    wave_o = __builtin_amdgcn_readfirstlane(wave_o);  // (uniform again)
+    tb_o = __builtin_amdgcn_readfirstlane(tb_o);
+    tw_o = __builtin_amdgcn_readfirstlane(tw_o);
+    r0_o = __builtin_amdgcn_readfirstlane(r0_o);
+    grp_o = __builtin_amdgcn_readfirstlane(grp_o);
+    chunk_o = __builtin_amdgcn_readfirstlane(chunk_o);
+  }
+  const int tid = tid_o, lane = lane_o, wave = wave_o, tb = tb_o, tw = tw_o, r0 = r0_o,
+            grp = grp_o, chunk = chunk_o;
+  const int lz = 0;
+  Dx3Layer Ly;
+  if constexpr (ML) {
+    Ly = ml->layer[li];
+  } else {
+    Ly = Dx3Layer{g.Wt, g.b3, g.vtap, g.bfull, g.out, g.yscale, g.C, g.nslab, g.nchunk,
+                  g.chunk_slabs, g.hlast};
+  }
+  const int tile = tb * T + tw + lz;
 
   // ---- DMA plan: piece k = wave + 8 i of each slab.  Halo pieces k < HPIECES: tile k /
   // (2 PLANE_KIB), plane (k / PLANE_KIB) % 2, canvas slots 32 (k % PLANE_KIB) .. +31 (lane:
@@ -385,10 +440,6 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   // the halo DMA addresses one slab at a time (a buffer resource per slab: 32-bit offsets
   // within a slab, so the whole copy may exceed 4 GiB -- config 5's 2048-patch batches)
   const int xs_rec = (int)(g.xs_slab < (int64_t)kDxInvalid ? g.xs_slab : (int64_t)kDxInvalid);
-  const uint32_t wslab = (uint32_t)(g.ngroup * L::WST);  // weight bytes per slab
-  const int64_t wbytes = (int64_t)g.nslab * wslab;
-  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)g.Wt, 0, (int)(wbytes < (int64_t)kDxInvalid ? wbytes : (int64_t)kDxInvalid), 0x00020000);
   // Per slot: the source byte offset of slab 0 (halo: per lane; an out-of-image slot gets
   // kDxOff, which stays past the buffer's end for every slab -- the buffer returns zeros, no
   // select in the loop) or within a slab (weights); the LDS offset within a stage; whether the
@@ -443,36 +494,10 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
       pbase[i] = (uint32_t)(grp * L::WST + k * 1024 + lane * 16);
     }
   }
-  // issue slot i's piece of slab s into stage st (a slab past the layer's reads zeros: the
-  // loop's last slab issues its "next" DMA unconditionally, into a stage nothing reads again)
-  auto dma = [&](int s, int st, int i) {
-    if (!pok[i]) return;
-    const bool halo = i < L::PH;
-    if (halo ? (IDF_DX3_ABLATE & 1) : (IDF_DX3_ABLATE & 4)) return;
-    // one call site for both kinds of piece (the LDS address formed from the __shared__ array
-    // itself): the host pass of hipcc drops the kernel's launch stub otherwise
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)((const char*)g.xs + (int64_t)s * g.xs_slab), 0, xs_rec, 0x00020000);
-    const uint32_t off = pbase[i] + (halo ? 0u : (uint32_t)(s * g.ngroup) * (uint32_t)L::WST);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(halo ? xr : wr,
-                                             (dx_lds_ptr_t)(lds + st * L::STAGE + plo[i]), 16,
-                                             off, 0, 0, 0);
-  };
-
-  // zeros for the odd tap's pair, and the epilogue's bias table (both outside the stages)
-  // the first slab's DMA first: the bias table's dependent global loads below then overlap its
-  // latency
-  if (s1 > s0) {
-#pragma unroll
-    for (int i = 0; i < L::PPW; ++i) dma(s0, 0, i);
-  }
   DX3_TL(0);
   for (int e = tid; e < NF * 512 / 16; e += kDxThreads) *(d4*)(lds + L::ZOFF + 16 * e) = d4{0.f, 0.f, 0.f, 0.f};
   DX3_PHASE(0, __builtin_amdgcn_s_memtime());
   DX3_PHASE(4, __builtin_amdgcn_s_memrealtime());
-  Dx3Tables<NF> tabs;  // loaded in the first slab, stored in the second (or after the loop)
-  DX3_PHASE(1, __builtin_amdgcn_s_memtime());
-  DX3_TL(1);
 
   // ---- the wave's canvas position: lane j's column base (gutter packing: j; segments: its
   // segment's base + its offset in the segment, = j mod 8) and the wave's first canvas row
@@ -515,6 +540,80 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   const int oAHG = L::WOFF + 2 * NF * 512 + j * 32 + (q & 1) * 16 + (q >> 1) * 3 * NF * 512;
   const bool zlane = q < 2;
   const char* zO = lds + L::ZOFF + j * 32 + (q & 1) * 16;
+
+  // ---- ML: the wave's rows (as the epilogue's) and the fused head's running sums, kept in
+  // registers across the layers from the head init on: per output o < n_head of pixel p,
+  // bias[o] then c = 0 .. c0 - 1 in order, fmaf(w[o][c], x[p][c], .) -- dx3_head_init_kernel's
+  // chain, so the sums carry the same bits as the split launches' HBM copy
+  if constexpr (ML) if (li == 0) {
+#pragma unroll
+    for (int m = 0; m < WR; ++m) hreg[m] = d4{0.f, 0.f, 0.f, 0.f};
+    if (g.nh > 0) {
+      const bool lane_ok0 = xj < g.Wd && ixj < g.nbx;
+#pragma unroll
+      for (int m = 0; m < WR; ++m) {
+        int iy = iyw, y = uyw + m - iyw * g.H;
+        if (g.gut) {
+          iy = udiv_s(uyw + m, g.hp);
+          y = uyw + m - iy * g.hp;
+        }
+        const int img = (dt.band * g.nby + iy) * g.nbx + ixj;
+        const bool ok = lane_ok0 && y < g.H && iy < g.nby && img < g.B;
+        if (ok && 4 * q < g.nh) {
+          const float* xr = ml->hx + (((int64_t)img * g.H + y) * g.Wd + xj) * ml->hld_x;
+          d4 h;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) h[i] = 4 * q + i < g.nh ? ml->hb[4 * q + i] : 0.0f;
+          for (int c = 0; c < ml->hc0; c += 4) {
+            const d4 xv = *(const d4*)(xr + c);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int o = 4 * q + i;
+              if (o < g.nh) {
+                const d4 wv = *(const d4*)(g.hw + (int64_t)o * g.ldhw + c);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) h[i] = __builtin_fmaf(wv[k], xv[k], h[i]);
+              }
+            }
+          }
+          hreg[m] = h;
+        }
+      }
+    }
+  }
+
+  // this block's slabs: a chunk of them (split launch), or all (ML: the chunks in order)
+  const int s0 = ML ? 0 : chunk * Ly.chunk_slabs;
+  const int s1 = ML ? Ly.nslab : min(Ly.nslab, s0 + Ly.chunk_slabs);
+  const uint32_t wslab = (uint32_t)(g.ngroup * L::WST);  // weight bytes per slab
+  const int64_t wbytes = (int64_t)Ly.nslab * wslab;
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)Ly.Wt, 0, (int)(wbytes < (int64_t)kDxInvalid ? wbytes : (int64_t)kDxInvalid), 0x00020000);
+  // issue slot i's piece of slab s into stage st (a slab past the layer's reads zeros: the
+  // loop's last slab issues its "next" DMA unconditionally, into a stage nothing reads again)
+  auto dma = [&](int s, int st, int i) {
+    if (!pok[i]) return;
+    const bool halo = i < L::PH;
+    if (halo ? (IDF_DX3_ABLATE & 1) : (IDF_DX3_ABLATE & 4)) return;
+    // one call site for both kinds of piece (the LDS address formed from the __shared__ array
+    // itself): the host pass of hipcc drops the kernel's launch stub otherwise
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)g.xs + (int64_t)s * g.xs_slab), 0, xs_rec, 0x00020000);
+    const uint32_t off = pbase[i] + (halo ? 0u : (uint32_t)(s * g.ngroup) * (uint32_t)L::WST);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(halo ? xr : wr,
+                                             (dx_lds_ptr_t)(lds + st * L::STAGE + plo[i]), 16,
+                                             off, 0, 0, 0);
+  };
+
+  // the first slab's DMA first: the tables' dependent global loads then overlap its latency
+  if (s1 > s0) {
+#pragma unroll
+    for (int i = 0; i < L::PPW; ++i) dma(s0, 0, i);
+  }
+  Dx3Tables<NF> tabs;  // loaded in the first slab, stored in the second (or after the loop)
+  DX3_PHASE(1, __builtin_amdgcn_s_memtime());
+  DX3_TL(1);
+
 
   d4 acc[WR][NF];
 #pragma unroll
@@ -587,8 +686,8 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
     if (!(IDF_DX3_ABLATE & 8)) __builtin_amdgcn_s_barrier();
     DX3_STAMP(s - s0, 1);
     if (s == s0) DX3_TL(2);
-    if (s == s0) tabs.load(g, grp, tid);
-    if (s == s0 + 1) tabs.store((float*)(lds + L::BOFF), (float*)(lds + L::HOFF), g, grp, tid);
+    if (s == s0) tabs.load(g, Ly, grp, tid);
+    if (s == s0 + 1) tabs.store((float*)(lds + L::BOFF), (float*)(lds + L::HOFF), g, Ly, grp, tid);
     __builtin_amdgcn_sched_barrier(0);
     const bool more = s + 1 < s1;
     const int nst = (s + 1 - s0) & 1;
@@ -807,8 +906,8 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   // the tables in LDS before any epilogue reads them: stored here when the loop had no second
   // slab, and ordered by one more barrier when no slab barrier followed the store
   if (s1 - s0 <= 1) {
-    if (s1 == s0) tabs.load(g, grp, tid);
-    tabs.store((float*)(lds + L::BOFF), (float*)(lds + L::HOFF), g, grp, tid);
+    if (s1 == s0) tabs.load(g, Ly, grp, tid);
+    tabs.store((float*)(lds + L::BOFF), (float*)(lds + L::HOFF), g, Ly, grp, tid);
   }
   if (s1 - s0 <= 2) __syncthreads();
 
@@ -821,10 +920,10 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   // bypass this CU's L1) -- no release / acquire fences, whose L2 write-back costs microseconds
   // per block.
   // (compiled only into the one-tile blocks: the host splits K only with T = 1)
-  if constexpr (T == 1) if (g.nchunk > 1) {
+  if constexpr (T == 1 && !ML) if (Ly.nchunk > 1) {
     constexpr int FR = kDxWaves * WR * NF;  // fragments per block
-    const uint32_t pb = (uint32_t)((tb * g.ngroup + grp) * g.nchunk) * (FR * 1024u);  // bytes
-    const int64_t pbytes = (int64_t)g.nblk_tiles * g.ngroup * g.nchunk * FR * 1024;
+    const uint32_t pb = (uint32_t)((tb * g.ngroup + grp) * Ly.nchunk) * (FR * 1024u);  // bytes
+    const int64_t pbytes = (int64_t)g.nblk_tiles * g.ngroup * Ly.nchunk * FR * 1024;
     const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(
         (void*)g.part, 0, (int)(pbytes < (int64_t)kDxInvalid ? pbytes : (int64_t)kDxInvalid), 0x00020000);
     auto poff = [&](int c, int m, int n) -> uint32_t {
@@ -841,7 +940,7 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
     if (tid == 0) {
       const uint32_t old = __hip_atomic_fetch_add(g.ctr + tb * g.ngroup + grp, 1u, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
-      const bool last = old == (uint32_t)(g.nchunk - 1);
+      const bool last = old == (uint32_t)(Ly.nchunk - 1);
       if (last)  // no other block touches it again in this launch: zero for the next one
         __hip_atomic_store(g.ctr + tb * g.ngroup + grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *last_flag = last;
@@ -860,7 +959,7 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
       for (int m = 0; m < WR; ++m)
 #pragma unroll
         for (int n = 0; n < NF; ++n)
-          pv[c][m][n] = (c < g.nchunk && c != chunk)
+          pv[c][m][n] = (c < Ly.nchunk && c != chunk)
                             ? __builtin_bit_cast(d4, __builtin_amdgcn_raw_buffer_load_b128(pr, poff(c, m, n), 0, 16))
                             : acc[m][n];
 #pragma unroll
@@ -870,7 +969,7 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
         d4 sum = pv[0][m][n];
 #pragma unroll
         for (int c = 1; c < 4; ++c)
-          if (c < g.nchunk) sum = sum + pv[c][m][n];
+          if (c < Ly.nchunk) sum = sum + pv[c][m][n];
         acc[m][n] = sum;
       }
     DX3_TL(4);
@@ -890,7 +989,7 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   const float* htab = (const float*)(lds + L::HOFF);
   const bool fh = g.nh > 0;
   bool out_ok = true;
-  const int zr = (g.C + g.N + 15) / 16 * 16, zend = zr < 16 * g.nslab_xs ? zr : 16 * g.nslab_xs;
+  const int zr = (Ly.C + g.N + 15) / 16 * 16, zend = zr < 16 * g.nslab_xs ? zr : 16 * g.nslab_xs;
   const bool lastg = grp == g.ngroup - 1;
   char* xsb = (char*)g.xs;
   // the wave's rows: image, y, pixel, whether the lane has an output there
@@ -915,7 +1014,8 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
 #pragma unroll
   for (int m = 0; m < WR; ++m) {
     hprev[m] = d4{0.f, 0.f, 0.f, 0.f};
-    if (fh && r_ok[m] && 4 * q < g.nh) hprev[m] = *(const d4*)(g.hacc + r_pix[m] * 16 + 4 * q);
+    if constexpr (ML) hprev[m] = hreg[m];  // (zeros where the head init left them)
+    else if (fh && r_ok[m] && 4 * q < g.nh) hprev[m] = *(const d4*)(g.hacc + r_pix[m] * 16 + 4 * q);
   }
   // outputs: bias, activation, the fp32 and split stores; acc[m][n] becomes the output (zeros
   // past N), which the head's shares below read
@@ -925,7 +1025,7 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
     if (!row_ok && !fh) continue;
     const int cls = bias_class(r_y[m], xj, g.H, g.Wd);
     const int64_t pix = r_pix[m];
-    float* dst = g.out + pix * g.ldo;
+    float* dst = Ly.out + pix * g.ldo;
 #pragma unroll
     for (int n = 0; n <= NF; ++n) {
       if (n == NF && !lastg) break;
@@ -936,7 +1036,7 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
         const d4 bv = *(const d4*)(btab + cls * (NF * 16) + nl);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const float t = acc[m][n][k] * g.yscale + bv[k];
+          const float t = acc[m][n][k] * Ly.yscale + bv[k];
           v[k] = act.tanh_ ? wact(t, g.act, g.slope) : act(t);
           if (!BF && row_ok) out_ok = out_ok && fabsf(v[k]) < kDxOutGuard;
         }
@@ -952,7 +1052,7 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
         for (int k = g.N - n0; k < 4; ++k) v[k] = 0.0f;
       }
       if (n < NF) acc[m][n] = v;
-      const int c = g.C + n0;  // split channel of v[0]; c % 4 == 0, so v stays in one slab
+      const int c = Ly.C + n0;  // split channel of v[0]; c % 4 == 0, so v stays in one slab
       if (row_ok && !(IDF_DX3_ABLATE & 128) && c < zend) {
         if constexpr (BF) {  // the bf16 copy, round to nearest even
           typedef __bf16 b4 __attribute__((ext_vector_type(4)));
@@ -1017,8 +1117,9 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
         d4 hv;
 #pragma unroll
         for (int i = 0; i < 4; ++i) hv[i] = prev[i] + r4[i];
-        if (!g.hlast) {
-          *ap = hv;
+        if (!Ly.hlast) {
+          if constexpr (ML) hreg[m] = hv;
+          else *ap = hv;
         } else {  // the complete head: its epilogue (flow_kernels.hip gemm_f32_kernel's)
           const int b_img = r_img[m];
           const int64_t hw_ = (int64_t)g.H * g.Wd, rem = (int64_t)r_y[m] * g.Wd + xj;
@@ -1051,6 +1152,24 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
   DX3_TL(5);
   DX3_PHASE(3, __builtin_amdgcn_s_memtime());
   DX3_PHASE(5, __builtin_amdgcn_s_memrealtime());
+  if constexpr (ML) {
+    // the layer's outputs (split copy, fp32 rows) stored and its LDS reads done before the next
+    // layer's DMA reads them / overwrites the stages and tables: every wave drained, one barrier
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  }  // layers
+}
+
+template <int NF, int WR, int PITCH, int PLANE_KIB, bool BF>
+__global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
+  dx3_block<NF, WR, PITCH, PLANE_KIB, BF, false>(g, nullptr);
+}
+
+// The fused DenseBlock: every layer of a block, one workgroup per tile (Dx3MLArgs)
+template <int NF, int PITCH, int PLANE_KIB, bool BF>
+__global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_block_kernel(Dx3Args g, Dx3MLArgs ml) {
+  dx3_block<NF, 16 / kDxWaves, PITCH, PLANE_KIB, BF, true>(g, &ml);
 }
 
 // Block-input split: XS channels [c0, c1) of every pixel from the fp32 rows x (ld_x floats),
@@ -1332,18 +1451,22 @@ extern "C" int idf_conv3x3_dxb_supported(int32_t H, int32_t W, int32_t N) {
   return dxb_plan_ok(dx3_plan(H, W, N, true)) ? 1 : 0;
 }
 
-// One dx3 launch, split-f16 (bf = false: xs the split copy) or bf16 (bf = true: xs the bf16
-// shadow).  xs_pix / xs_slab / xs_bytes: the buffer's pixel and slab strides and size, bytes.
-static int dx3_run(void* stream, bool bf, int32_t B, int32_t H, int32_t W, int32_t C, uint16_t* xs,
-                   int64_t xs_pix, int64_t xs_slab, int64_t xs_bytes, int32_t nslab_xs,
-                   const uint16_t* w, int32_t nft, float yscale, const float* b3,
-                   const float* vtap, int32_t ldv, const float* bfull, int32_t N, float* out,
-                   int64_t ld_out, int32_t act, float slope, uint32_t* d_flag, void* d_workspace,
-                   int64_t workspace_bytes, const IdfDx3Head* head) {
-  if (B <= 0 || H <= 0 || W <= 0 || N <= 0) return IDF_OK;
+// A dx3 launch's arguments, split-f16 (bf = false: xs the split copy) or bf16 (bf = true: xs the
+// bf16 shadow).  xs_pix / xs_slab / xs_bytes: the buffer's pixel and slab strides and size,
+// bytes.  ml: the fused DenseBlock's first layer (no split-K workspace; one tile per block).
+static int dx3_args(Dx3Args& g, Dx3Launch& sh, bool ml, bool bf, int32_t B, int32_t H, int32_t W,
+                    int32_t C, uint16_t* xs, int64_t xs_pix, int64_t xs_slab, int64_t xs_bytes,
+                    int32_t nslab_xs, const uint16_t* w, int32_t nft, float yscale, const float* b3,
+                    const float* vtap, int32_t ldv, const float* bfull, int32_t N, float* out,
+                    int64_t ld_out, int32_t act, float slope, uint32_t* d_flag, void* d_workspace,
+                    int64_t workspace_bytes, const IdfDx3Head* head) {
   if (C <= 0 || (C & 3) || !w || !xs || !out || !b3) return IDF_ERR_ARG;
-  const Dx3Launch sh = dx3_launch_shape(B, H, W, C, N, bf);
+  sh = dx3_launch_shape(B, H, W, C, N, bf);
   if (!sh.pl.ok || (bf && !dxb_plan_ok(sh.pl))) return IDF_ERR_UNSUPPORTED;
+  if (ml) {  // one tile per workgroup, every chunk in it
+    sh.T = 1;
+    sh.nblk_tiles = (int)sh.ntiles;
+  }
   // the weights hold exactly the kernel's fragments: ngroup groups of nf, nft = ngroup * nf
   if (nft != sh.pl.ngroup * sh.pl.nf) return IDF_ERR_ARG;
   if (vtap && (!bfull || ldv < N)) return IDF_ERR_ARG;
@@ -1353,14 +1476,14 @@ static int dx3_run(void* stream, bool bf, int32_t B, int32_t H, int32_t W, int32
   // 32-bit buffer offsets within a slab, and kDxOff past the end of every slab: one slab of the
   // copy must span < 2 GiB (P < 32M pixels)
   if (xs_slab >= (int64_t)kDxOff) return IDF_ERR_UNSUPPORTED;
-  const int64_t nblk = (int64_t)sh.nblk_tiles * sh.pl.ngroup * sh.nchunk;
+  const int64_t nblk = (int64_t)sh.nblk_tiles * sh.pl.ngroup * (ml ? 1 : sh.nchunk);
   if (sh.ntiles >= (1 << 20) || nblk >= (1 << 20)) return IDF_ERR_UNSUPPORTED;  // udiv_s operands
-  // split K: the kernel addresses the partial sums with 32-bit offsets through one buffer
-  // resource (kDxInvalid records at most), nblk blocks x fragments x 1 KiB
-  if (sh.nchunk > 1 && nblk * (int64_t)(kDxWaves * (16 / kDxWaves) * sh.pl.nf) * 1024 >= (int64_t)kDxInvalid)
-    return IDF_ERR_UNSUPPORTED;
-  Dx3Args g = {};
-  if (sh.nchunk > 1) {
+  g = {};
+  if (sh.nchunk > 1 && !ml) {
+    // split K: the kernel addresses the partial sums with 32-bit offsets through one buffer
+    // resource (kDxInvalid records at most), nblk blocks x fragments x 1 KiB
+    if (nblk * (int64_t)(kDxWaves * (16 / kDxWaves) * sh.pl.nf) * 1024 >= (int64_t)kDxInvalid)
+      return IDF_ERR_UNSUPPORTED;
     const int64_t cb = idf_conv3x3_dx3_counter_bytes(B, H, W, N);
     if (!d_workspace || (uintptr_t)d_workspace % 256 || workspace_bytes < cb + sh.part_bytes)
       return IDF_ERR_WORKSPACE;
@@ -1384,11 +1507,11 @@ static int dx3_run(void* stream, bool bf, int32_t B, int32_t H, int32_t W, int32
   g.out = out; g.ldo = ld_out; g.yscale = yscale; g.flag = d_flag;
   if (head && head->n_head > 0) {
     // one block writes a pixel's running head sums: one output group only; <= 16 outputs
-    if (head->n_head > 16 || sh.pl.ngroup != 1 || !head->w || !head->acc || head->ldw < C + N ||
-        (uintptr_t)head->acc % 16)
+    if (head->n_head > 16 || sh.pl.ngroup != 1 || !head->w || (!head->acc && !ml) ||
+        head->ldw < C + N || (uintptr_t)head->acc % 16)
       return IDF_ERR_ARG;
     const IdfHeadOut& o = head->out;
-    if (head->last) {
+    if (head->last || ml) {
       if (o.mode == IDF_EPI_PRIOR ? (!o.mean || !o.logscale || !o.scale || o.n_mean < 0 ||
                                      2 * o.n_mean != head->n_head)
                                   : (!o.out || ((o.mode == IDF_EPI_COUPLE_ADD ||
@@ -1402,6 +1525,24 @@ static int dx3_run(void* stream, bool bf, int32_t B, int32_t H, int32_t W, int32
   } else if (head && head->skip_f32) {
     g.skip_f32 = 1;
   }
+  return IDF_OK;
+}
+
+// One dx3 launch (one layer).
+static int dx3_run(void* stream, bool bf, int32_t B, int32_t H, int32_t W, int32_t C, uint16_t* xs,
+                   int64_t xs_pix, int64_t xs_slab, int64_t xs_bytes, int32_t nslab_xs,
+                   const uint16_t* w, int32_t nft, float yscale, const float* b3,
+                   const float* vtap, int32_t ldv, const float* bfull, int32_t N, float* out,
+                   int64_t ld_out, int32_t act, float slope, uint32_t* d_flag, void* d_workspace,
+                   int64_t workspace_bytes, const IdfDx3Head* head) {
+  if (B <= 0 || H <= 0 || W <= 0 || N <= 0) return IDF_OK;
+  Dx3Args g;
+  Dx3Launch sh;
+  if (int rc = dx3_args(g, sh, false, bf, B, H, W, C, xs, xs_pix, xs_slab, xs_bytes, nslab_xs, w,
+                        nft, yscale, b3, vtap, ldv, bfull, N, out, ld_out, act, slope, d_flag,
+                        d_workspace, workspace_bytes, head))
+    return rc;
+  const int64_t nblk = (int64_t)sh.nblk_tiles * sh.pl.ngroup * sh.nchunk;
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)nblk), blk(kDxThreads);
 #define IDF_DX3_GO(nf_, wr_, pitch_, kib_) \
@@ -1449,6 +1590,95 @@ static int dx3_run(void* stream, bool bf, int32_t B, int32_t H, int32_t W, int32
 #undef IDF_DX3_NF
 #undef IDF_DX3_GO
 #undef IDF_DXB_GO
+  return idf_last_error();
+}
+
+
+// tiles that hold whole images (no halo crosses a tile: a tile's layers need only its own earlier
+// layers): one image per tile (16-wide images up to 16 rows) or the 4- / 8-wide segments, whose
+// canvases hold whole images with zero gutters.  Not the split-K geometries (imagenet64's 8 x 8
+// level): there one workgroup per tile runs every chunk of every layer in turn, measured 473 vs
+// 308 us per DenseBlock (1.54x the per-layer launches' latency, bench -3%, profiles/r06/fused/).
+static bool dx3_self_contained(const Dx3Plan& p, int H, int W) {
+  if (!p.ok || p.gut || p.ngroup != 1 || p.split > 1) return false;
+  if (W % 16 == 0) return W == 16 && H <= 16;
+  return p.nby > 1 || H <= 16;
+}
+
+extern "C" int idf_dx3_block_supported(int32_t H, int32_t W, int32_t N, int32_t bf) {
+  const Dx3Plan p = dx3_plan(H, W, N, bf != 0);
+  if (bf && !dxb_plan_ok(p)) return 0;
+  return dx3_self_contained(p, H, W) && (p.pitch == 18 || p.pitch == 10 || (!bf && p.pitch == 6));
+}
+
+int idf_dx3_block_launch(void* stream, const IdfDx3BlockDesc* d) {
+  if (!d || d->nlayers < 1 || d->nlayers > kDxMaxLayers || !d->C || !d->w || !d->b3 || !d->feat)
+    return IDF_ERR_ARG;
+  if (d->B <= 0 || d->H <= 0 || d->W <= 0 || d->N <= 0) return IDF_OK;
+  if (!idf_dx3_block_supported(d->H, d->W, d->N, d->bf)) return IDF_ERR_UNSUPPORTED;
+  const bool bf = d->bf != 0;
+  const int64_t P = (int64_t)d->B * d->H * d->W;
+  const int64_t xs_slab = bf ? P * 32 : 2 * P * 32;
+  const int64_t xs_bytes = bf ? idf_dxb_bytes(P, 16 * d->nslab_xs) : idf_dx3_split_bytes(P, 16 * d->nslab_xs);
+  const bool fh = d->head && d->head->n_head > 0;
+  if (fh && (!d->hx || !d->hb || d->hc0 < 0 || d->hc0 > 64 || (d->hc0 & 3) || (d->hld_x & 3) ||
+             (uintptr_t)d->hx % 16 || (uintptr_t)d->head->w % 16 || (d->head->ldw & 3)))
+    return IDF_ERR_ARG;
+  Dx3Args g;
+  Dx3Launch sh;
+  IdfDx3Head h0 = {};
+  if (fh) {
+    h0 = *d->head;
+    h0.last = d->nlayers == 1;
+  }
+  // the block's fields, checked and set from layer 0 (the plan depends on H, W, N only)
+  if (int rc = dx3_args(g, sh, true, bf, d->B, d->H, d->W, d->C[0], d->xs, 32, xs_slab, xs_bytes,
+                        d->nslab_xs, d->w[0], d->nft, bf ? 1.0f : d->yscale[0], d->b3[0],
+                        d->vtap ? d->vtap[0] : nullptr, d->ldv, d->bfull ? d->bfull[0] : nullptr,
+                        d->N, d->feat + d->C[0], d->ld_feat, d->act, d->slope, bf ? nullptr : d->flag,
+                        nullptr, 0, fh ? &h0 : (d->head ? d->head : nullptr)))
+    return rc;
+  Dx3MLArgs ml = {};
+  ml.nlayers = d->nlayers;
+  for (int i = 0; i < d->nlayers; ++i) {
+    const int C = d->C[i];
+    if (C <= 0 || (C & 3) || !d->w[i] || !d->b3[i] || (C + 15) / 16 > d->nslab_xs) return IDF_ERR_ARG;
+    if (d->vtap && d->vtap[i] && (!d->bfull || !d->bfull[i])) return IDF_ERR_ARG;
+    if (fh && d->head->ldw < C + d->N) return IDF_ERR_ARG;
+    const Dx3Launch li = dx3_launch_shape(d->B, d->H, d->W, C, d->N, bf);
+    Dx3Layer& L = ml.layer[i];
+    L.Wt = d->w[i]; L.b3 = d->b3[i]; L.vtap = d->vtap ? d->vtap[i] : nullptr;
+    L.bfull = d->bfull ? d->bfull[i] : nullptr; L.out = d->feat + C;
+    L.yscale = bf ? 1.0f : d->yscale[i];
+    L.C = C; L.nslab = li.nslab; L.nchunk = li.nchunk; L.chunk_slabs = li.chunk_slabs;
+    L.hlast = fh && i == d->nlayers - 1;
+  }
+  if (fh) {
+    ml.hx = d->hx; ml.hld_x = d->hld_x; ml.hc0 = d->hc0; ml.hb = d->hb;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)sh.ntiles), blk(kDxThreads);
+#define IDF_DX3B_GO(nf_, pitch_, kib_, bf_) \
+  hipLaunchKernelGGL((conv3_dx3_block_kernel<nf_, pitch_, kib_, bf_>), grid, blk, 0, s, g, ml)
+#define IDF_DX3B_NF(pitch_, kib_, bf_)                              \
+  switch (sh.pl.nf) {                                              \
+    case 1: IDF_DX3B_GO(1, pitch_, kib_, bf_); break;              \
+    case 2: IDF_DX3B_GO(2, pitch_, kib_, bf_); break;              \
+    case 3: IDF_DX3B_GO(3, pitch_, kib_, bf_); break;              \
+    default: if (!bf_) IDF_DX3B_GO(4, pitch_, kib_, false); break; \
+  }
+  if (bf) {
+    if (sh.pl.pitch == 18) IDF_DX3B_NF(18, 11, true)
+    else IDF_DX3B_NF(10, 13, true)
+  } else if (sh.pl.pitch == 18) {
+    IDF_DX3B_NF(18, 11, false)
+  } else if (sh.pl.pitch == 10) {
+    IDF_DX3B_NF(10, 13, false)
+  } else {
+    IDF_DX3B_NF(6, 19, false)
+  }
+#undef IDF_DX3B_NF
+#undef IDF_DX3B_GO
   return idf_last_error();
 }
 

@@ -706,6 +706,11 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
     const int nft = (blk->g_pad + 15) / 16, nf = nft < 4 ? nft : 4;
     return (nft + nf - 1) / nf * nf;
   }();
+  // the fused DenseBlock (IdfDenseBlock.fuse_layers): every layer in one launch, one workgroup
+  // per tile, where the tiles hold whole images (conv3_dx3.hip conv3_dx3_block_kernel) -- the
+  // per-layer launches' bits, with the fused head's sums in registers (no head init launch)
+  const bool fused = blk->fuse_layers && (dx3 || dxb) && n_dx3 == blk->depth && blk->depth >= 1 &&
+                     blk->depth <= 16 && idf_dx3_block_supported(H, W, blk->g_pad, dxb ? 1 : 0);
   if (dx3 || dxb) {
     const int64_t avail = ws_floats * 4;
     if (pl.bytes > avail || (uintptr_t)tmp % 256) return IDF_ERR_WORKSPACE;
@@ -723,13 +728,49 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
                                       blk->range_flag, need > 0 ? (uint32_t*)dws : nullptr,
                                       need > 0 ? (int32_t)(ctr / 4) : 0);
     if (rc) return rc;
-    if (hacc) {
+    if (hacc && !fused) {
       rc = idf_dx3_head_init(stream, P, blk->k_in[0], feat, ld_feat, blk->wh, blk->ldwh, blk->bh,
                              blk->n_head, hacc);
       if (rc) return rc;
     }
   }
-  for (int i = 0; i < blk->depth; ++i) {
+  if (fused) {
+    int32_t C[16];
+    const uint16_t* w[16];
+    float ys[16];
+    const float *b3[16], *vt[16], *bfu[16];
+    double fl = 0.0;
+    for (int i = 0; i < blk->depth; ++i) {
+      C[i] = blk->k_in[i];
+      w[i] = dxb ? blk->dxb_w[i] : blk->dx3_w[i];
+      ys[i] = dxb ? 1.0f : blk->dx3_yscale[i];
+      b3[i] = blk->b3[i];
+      vt[i] = blk->vtap[i];
+      bfu[i] = blk->bfull[i];
+      fl += 2.0 * P * 9.0 * blk->c_real[i] * blk->g_real[i];
+    }
+    IdfDx3Head hd = {};
+    if (hacc) {
+      hd.w = blk->wh; hd.ldw = blk->ldwh; hd.n_head = blk->n_head; hd.acc = nullptr;
+      hd.last = 1;
+      hd.skip_f32 = blk->keep_feat ? 0 : 1;
+      hd.out = *head;
+    }
+    IdfDx3BlockDesc d = {};
+    d.bf = dxb ? 1 : 0;
+    d.B = B; d.H = H; d.W = W; d.nlayers = blk->depth; d.N = blk->g_pad; d.nft = dx3_nft;
+    d.ldv = blk->ldv; d.act = blk->act; d.nslab_xs = nslab_xs; d.slope = blk->slope;
+    d.xs = xs; d.C = C; d.w = w; d.yscale = ys; d.b3 = b3;
+    d.vtap = blk->vtap[0] ? vt : nullptr; d.bfull = blk->vtap[0] ? bfu : nullptr;
+    d.feat = feat; d.ld_feat = ld_feat; d.flag = dxb ? nullptr : blk->range_flag;
+    d.head = hacc ? &hd : nullptr;
+    d.hx = feat; d.hld_x = ld_feat; d.hc0 = blk->k_in[0]; d.hb = blk->bh;
+    timer_mark(timer, s, IDF_TAG_CONV3X3, fl, true);
+    const int rc = idf_dx3_block_launch(stream, &d);
+    timer_mark(timer, s, 0, 0, false);
+    if (rc) return rc;
+  }
+  for (int i = 0; i < (fused ? 0 : blk->depth); ++i) {
     const int c = blk->k_in[i];
     IdfDx3Head hd = {};
     if (hacc) {

@@ -5,6 +5,33 @@
 
 #include "../../include/idf_codec.h"
 
+// The fused DenseBlock launch on the direct convs (conv3_dx3.hip conv3_dx3_block_kernel; used
+// by flow_kernels.hip dense_block_run): every layer of a block in one launch, one workgroup per
+// tile, for geometries whose tiles hold whole images.  Bit for bit the same outputs, split
+// copy, fused-head results and range-guard flag as one idf_conv3x3_dx3 / dxb launch per layer.
+struct IdfDx3BlockDesc {
+  int32_t bf;                    // 0: split-f16 (dx3), 1: bf16 (dxb)
+  int32_t B, H, W, nlayers, N, nft, ldv, act, nslab_xs;
+  float slope;
+  uint16_t* xs;                  // the block's split (bf16) feature copy
+  const int32_t* C;              // [nlayers] input channels
+  const uint16_t* const* w;      // [nlayers] dx3 / dxb weights
+  const float* yscale;           // [nlayers] (dx3)
+  const float* const* b3;
+  const float* const* vtap;
+  const float* const* bfull;
+  float* feat;                   // layer i's fp32 outputs at feat + C[i] (rows of ld_feat)
+  int64_t ld_feat;
+  uint32_t* flag;                // range guard (dx3)
+  const IdfDx3Head* head;        // fused head: w / ldw / n_head / skip_f32 / out (acc unused),
+                                 // the sums kept in registers; nullptr: none
+  const float* hx;               // the head init's block input (fp32 rows of hld_x), hc0 channels
+  int64_t hld_x;
+  int32_t hc0;
+  const float* hb;               // the head bias
+};
+int idf_dx3_block_launch(void* stream, const IdfDx3BlockDesc* d);
+
 // marker written by rans_cdf_freq for scale == 0 (freq can never be INT32_MIN)
 #define IDF_FREQ_SCALE_ZERO ((int32_t)0x80000000)
 

@@ -27,6 +27,7 @@
 namespace idf {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 
 constexpr int kMaxTaps = 16;
 
@@ -51,6 +52,11 @@ struct ConvTapsArgs {
   float slope;
   int64_t P;  // B * Hc * Wc
   int32_t m_tiles, n_tiles;
+  // X3 (split-f16 products): W holds per 4 channels (wh[4], wl[4]) f16 of w * 2^k (the same 16
+  // bytes as 4 fp32 weights), yscale = 2^-k; flag: bit 0 set when an input value is NaN or
+  // |x| >= 32768 (the f16 pairs' range; the caller recomputes in fp32)
+  float yscale;
+  uint32_t* flag;
 };
 
 __device__ __forceinline__ float vq_act(float v, int act, float slope) {
@@ -60,7 +66,11 @@ __device__ __forceinline__ float vq_act(float v, int act, float slope) {
   return v;
 }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N>
+// X3 = true: the same GEMM with every fp32 product as three f16 products on
+// v_mfma_f32_16x16x16_f16 (x = xh + xl split when the tile is staged, the weights pre-split on
+// the host): xh.wh + xl.wh + xh.wl per k-step, fp32 accumulation -- the split-f16 arithmetic of
+// the flow's dx3 / wx3 convs, 1/16 of the MFMA cycles of the fp32 16x16x4 steps it replaces.
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool X3>
 __global__ void __launch_bounds__(256) conv_taps_kernel(ConvTapsArgs g) {
   constexpr int BK = 16;
   constexpr int LDS_LD = BK + 8;  // conflict-free b128 fragment reads
@@ -121,9 +131,23 @@ __global__ void __launch_bounds__(256) conv_taps_kernel(ConvTapsArgs g) {
       }
     }
   };
+  bool in_ok = true;
   auto store_chunk = [&](int buf) {
 #pragma unroll
-    for (int j = 0; j < A_PER_T; ++j) *(f4*)&As[buf][a_row[j]][4 * a_kq[j]] = ra[j];
+    for (int j = 0; j < A_PER_T; ++j) {
+      if constexpr (X3) {  // (xh[4], xl[4]) in the 16 bytes of the 4 fp32 values
+        const f4 v = ra[j];
+        in_ok = in_ok && fabsf(v[0]) < 32768.0f && fabsf(v[1]) < 32768.0f &&
+                fabsf(v[2]) < 32768.0f && fabsf(v[3]) < 32768.0f;
+        const h4 hi = __builtin_convertvector(v, h4);
+        const h4 lo = __builtin_convertvector(v - __builtin_convertvector(hi, f4), h4);
+        typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+        *(h8*)&As[buf][a_row[j]][4 * a_kq[j]] =
+            h8{hi[0], hi[1], hi[2], hi[3], lo[0], lo[1], lo[2], lo[3]};
+      } else {
+        *(f4*)&As[buf][a_row[j]][4 * a_kq[j]] = ra[j];
+      }
+    }
 #pragma unroll
     for (int j = 0; j < B_PER_T; ++j) {
       const int f = tid + 256 * j;
@@ -149,13 +173,31 @@ __global__ void __launch_bounds__(256) conv_taps_kernel(ConvTapsArgs g) {
     for (int i = 0; i < FM; ++i) fa[i] = *(const f4*)&As[buf][wm * WTM + i * 16 + lr][lk];
 #pragma unroll
     for (int j = 0; j < FN; ++j) fb[j] = *(const f4*)&Bs[buf][wn * WTN + j * 16 + lr][lk];
+    if constexpr (X3) {
+      // lane: row lr, k = lk .. lk + 3 -- the A / B layout of v_mfma_f32_16x16x16_f16
+      typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+      for (int i = 0; i < FM; ++i) {
+        const h8 a8 = __builtin_bit_cast(h8, fa[i]);
+        const h4 ah = h4{a8[0], a8[1], a8[2], a8[3]}, al = h4{a8[4], a8[5], a8[6], a8[7]};
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+        for (int j = 0; j < FN; ++j) {
+          const h8 b8 = __builtin_bit_cast(h8, fb[j]);
+          const h4 bh = h4{b8[0], b8[1], b8[2], b8[3]}, bl = h4{b8[4], b8[5], b8[6], b8[7]};
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bh, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x16f16(al, bh, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bl, acc[i][j], 0, 0, 0);
+        }
+      }
+    } else {
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][t], fb[j][t], acc[i][j], 0, 0, 0);
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][t], fb[j][t], acc[i][j], 0, 0, 0);
+    }
     if (kc + 1 < nk) store_chunk(buf ^ 1);
     __syncthreads();
   }
@@ -184,21 +226,22 @@ __global__ void __launch_bounds__(256) conv_taps_kernel(ConvTapsArgs g) {
       for (int j = 0; j < FN; ++j) {
         const int n = n0 + wn * WTN + j * 16 + lr;
         if (n >= g.N) continue;
-        float v = acc[i][j][r] + bv[j];
+        float v = (X3 ? acc[i][j][r] * g.yscale : acc[i][j][r]) + bv[j];
         if (g.res) v = g.res[o * g.ldr + n] + v;  // ResBlock: x + resblock(x) (nnblock.py:81-82)
         g.out[o * g.ldo + n] = vq_act(v, g.act, g.slope);
       }
     }
+  if (X3 && !in_ok && g.flag) atomicOr(g.flag, 1u);
 }
 
-template <int BN>
+template <int BN, bool X3>
 static int launch_taps(ConvTapsArgs a, hipStream_t s) {
   constexpr int WN = BN >= 64 ? 2 : 1;
   constexpr int WM = 4 / WN;
   constexpr int BM = 64;
   a.m_tiles = (int)((a.P + BM - 1) / BM);
   a.n_tiles = (a.N + BN - 1) / BN;
-  hipLaunchKernelGGL((conv_taps_kernel<BM, BN, WM, WN>), dim3((unsigned)(a.m_tiles * a.n_tiles)),
+  hipLaunchKernelGGL((conv_taps_kernel<BM, BN, WM, WN, X3>), dim3((unsigned)(a.m_tiles * a.n_tiles)),
                      dim3(256), 0, s, a);
   return idf_last_error();
 }
@@ -508,15 +551,16 @@ using namespace idf;
 
 extern "C" {
 
-int idf_conv_taps_f32(void* stream, int32_t B, int32_t Hi, int32_t Wi, int32_t C, const float* x,
-                      int64_t ld_x, int32_t Hc, int32_t Wc, int32_t isy, int32_t isx, int32_t ntaps,
-                      const int32_t* dy, const int32_t* dx, const float* w, int32_t ldw,
-                      int32_t n_alloc, const float* bias, int32_t N, float* out, int64_t ld_out,
-                      int32_t Ho, int32_t Wo, int32_t osy, int32_t osx, int32_t oy0, int32_t ox0,
-                      const float* res, int64_t ld_res, int32_t act, float slope) {
+static int conv_taps_run(bool x3, void* stream, int32_t B, int32_t Hi, int32_t Wi, int32_t C,
+                         const float* x, int64_t ld_x, int32_t Hc, int32_t Wc, int32_t isy,
+                         int32_t isx, int32_t ntaps, const int32_t* dy, const int32_t* dx,
+                         const float* w, int32_t ldw, int32_t n_alloc, const float* bias, int32_t N,
+                         float* out, int64_t ld_out, int32_t Ho, int32_t Wo, int32_t osy,
+                         int32_t osx, int32_t oy0, int32_t ox0, const float* res, int64_t ld_res,
+                         int32_t act, float slope, float yscale, uint32_t* d_flag) {
   if (B <= 0 || Hc <= 0 || Wc <= 0 || N <= 0) return IDF_OK;
   if (ntaps < 1 || ntaps > kMaxTaps || C <= 0 || (C & 3) || (ld_x & 3) || (ldw & 15) ||
-      ldw < ((C + 15) / 16) * 16 || !dy || !dx)
+      ldw < ((C + 15) / 16) * 16 || !dy || !dx || !x || !w || !out)
     return IDF_ERR_ARG;
   ConvTapsArgs a = {};
   a.X = x; a.ldx = ld_x; a.B = B; a.Hi = Hi; a.Wi = Wi; a.C = C; a.Hc = Hc; a.Wc = Wc;
@@ -528,14 +572,43 @@ int idf_conv_taps_f32(void* stream, int32_t B, int32_t Hi, int32_t Wi, int32_t C
   a.W = w; a.ldw = ldw; a.bias = bias; a.N = N; a.out = out; a.ldo = ld_out;
   a.Ho = Ho; a.Wo = Wo; a.osy = osy; a.osx = osx; a.oy0 = oy0; a.ox0 = ox0;
   a.res = res; a.ldr = ld_res; a.act = act; a.slope = slope;
+  a.yscale = yscale; a.flag = d_flag;
   a.P = (int64_t)B * Hc * Wc;
   if (a.P >= ((int64_t)1 << 31)) return IDF_ERR_UNSUPPORTED;  // 32-bit pixel decomposition
   const int bn = N <= 32 ? 32 : (N <= 64 ? 64 : 128);
   if (n_alloc < ((N + bn - 1) / bn) * bn) return IDF_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-  if (bn == 32) return launch_taps<32>(a, s);
-  if (bn == 64) return launch_taps<64>(a, s);
-  return launch_taps<128>(a, s);
+  if (x3) {
+    if (bn == 32) return launch_taps<32, true>(a, s);
+    if (bn == 64) return launch_taps<64, true>(a, s);
+    return launch_taps<128, true>(a, s);
+  }
+  if (bn == 32) return launch_taps<32, false>(a, s);
+  if (bn == 64) return launch_taps<64, false>(a, s);
+  return launch_taps<128, false>(a, s);
+}
+
+int idf_conv_taps_f32(void* stream, int32_t B, int32_t Hi, int32_t Wi, int32_t C, const float* x,
+                      int64_t ld_x, int32_t Hc, int32_t Wc, int32_t isy, int32_t isx, int32_t ntaps,
+                      const int32_t* dy, const int32_t* dx, const float* w, int32_t ldw,
+                      int32_t n_alloc, const float* bias, int32_t N, float* out, int64_t ld_out,
+                      int32_t Ho, int32_t Wo, int32_t osy, int32_t osx, int32_t oy0, int32_t ox0,
+                      const float* res, int64_t ld_res, int32_t act, float slope) {
+  return conv_taps_run(false, stream, B, Hi, Wi, C, x, ld_x, Hc, Wc, isy, isx, ntaps, dy, dx, w,
+                       ldw, n_alloc, bias, N, out, ld_out, Ho, Wo, osy, osx, oy0, ox0, res, ld_res,
+                       act, slope, 1.0f, nullptr);
+}
+
+int idf_conv_taps_x3(void* stream, int32_t B, int32_t Hi, int32_t Wi, int32_t C, const float* x,
+                     int64_t ld_x, int32_t Hc, int32_t Wc, int32_t isy, int32_t isx, int32_t ntaps,
+                     const int32_t* dy, const int32_t* dx, const uint16_t* w, int32_t ldw,
+                     int32_t n_alloc, float yscale, const float* bias, int32_t N, float* out,
+                     int64_t ld_out, int32_t Ho, int32_t Wo, int32_t osy, int32_t osx, int32_t oy0,
+                     int32_t ox0, const float* res, int64_t ld_res, int32_t act, float slope,
+                     uint32_t* d_flag) {
+  return conv_taps_run(true, stream, B, Hi, Wi, C, x, ld_x, Hc, Wc, isy, isx, ntaps, dy, dx,
+                       (const float*)w, ldw, n_alloc, bias, N, out, ld_out, Ho, Wo, osy, osx, oy0,
+                       ox0, res, ld_res, act, slope, yscale, d_flag);
 }
 
 int idf_conv_taps_n_alloc(int32_t N) {

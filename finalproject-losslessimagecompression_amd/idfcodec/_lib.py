@@ -57,7 +57,7 @@ class IdfDenseBlock(ctypes.Structure):
         ("wx3", i32), ("wx3_yscale", f32 * MAX_DEPTH), ("wx3_u", P * MAX_DEPTH), ("range_flag", P),
         ("dx3", i32), ("dx3_yscale", f32 * MAX_DEPTH), ("dx3_w", P * MAX_DEPTH),
         ("fuse_head", i32), ("keep_feat", i32),
-        ("dxb", i32), ("dxb_w", P * MAX_DEPTH),
+        ("dxb", i32), ("dxb_w", P * MAX_DEPTH), ("fuse_layers", i32),
     ]
 
 
@@ -97,6 +97,7 @@ SIGNATURES = {
     "idf_rans_part1_selfcheck": (ctypes.c_int, [P, u64, u64, P]),
     "idf_dense_block_f32": (ctypes.c_int, [P, P, i32, i32, i32, P, i64, P, i64, P]),
     "idf_dense_block_dx3_tmp_bytes": (i64, [P, i32, i32, i32]),
+    "idf_dx3_block_supported": (ctypes.c_int, [i32, i32, i32, i32]),
     "idf_timer_create": (P, [i32]),
     "idf_timer_destroy": (None, [P]),
     "idf_timer_reset": (None, [P]),
@@ -150,6 +151,9 @@ SIGNATURES = {
     "idf_conv_taps_f32": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, i32, i32, i32, i32, i32, P,
                                          P, P, i32, i32, P, i32, P, i64, i32, i32, i32, i32, i32,
                                          i32, P, i64, i32, f32]),
+    "idf_conv_taps_x3": (ctypes.c_int, [P, i32, i32, i32, i32, P, i64, i32, i32, i32, i32, i32, P,
+                                        P, P, i32, i32, f32, P, i32, P, i64, i32, i32, i32, i32,
+                                        i32, i32, P, i64, i32, f32, P]),
     "idf_vq_norms": (ctypes.c_int, [P, i32, i32, P, i32, P]),
     "idf_vq_argmin": (ctypes.c_int, [P, i64, i32, P, i64, P, i32, i32, P, P]),
     "idf_vq_argmin_ws": (ctypes.c_int, [P, i64, i32, P, i64, P, i32, i32, P, P, P, i64]),

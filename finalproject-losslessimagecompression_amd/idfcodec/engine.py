@@ -60,6 +60,16 @@ DX3 = os.environ.get("IDF_DX3", "1") != "0"
 # of the conv arithmetic the mode names (the head's sums run in another order than the GEMM's):
 # on in modes 'dx3' and 'dxb', off in 'dx3w16', decided by the block geometry alone -- no switch,
 # so an encoder and its decoder cannot disagree on it.
+# Blocks whose layers all run on dx3 / dxb at a geometry whose tiles hold whole images (the
+# 16x16 and 8x8 levels, config 4's 4x4 patches) run as ONE launch per DenseBlock, a workgroup per
+# tile looping over the layers (IdfDenseBlock.fuse_layers, conv3_dx3_block_kernel): bit for bit
+# the per-layer launches' results, so not part of the bitstream; IDF_FUSE_LAYERS=0 keeps one
+# launch per layer (A/B timing, the equivalence tests).
+# IDF_FUSE_LAYERS: "1" every level the kernel takes, "0" none, or a comma list of level heights
+# (e.g. "8,4").
+_FL = os.environ.get("IDF_FUSE_LAYERS", "1")
+FUSE_LAYERS = _FL != "0"
+FUSE_LEVELS = None if _FL in ("0", "1") else {int(v) for v in _FL.split(",") if v}
 # bf16 engines (configs naming bf16 coupling convs) run their DenseLayers as the bf16 direct
 # conv (conv mode "dxb", idf_conv3x3_dxb: the dx3 kernel's tiling and LDS-DMA with one bf16
 # product per tap) where the level geometry allows, conv3_bf16.hip ("bf16", round 4's) elsewhere
@@ -137,6 +147,7 @@ class DeviceBlock:
             d.wb16[i] = u.data_ptr()
         d.dxb = 1 if (d.bf16 and self.dxb_w and DXB) else 0
         d.fuse_head = 1 if (d.dx3 or d.dxb) else 0
+        d.fuse_layers = 1 if FUSE_LAYERS else 0
         for i, u in enumerate(self.dxb_w):
             d.dxb_w[i] = u.data_ptr()
         d.ldv = packed.g_alloc
@@ -286,6 +297,10 @@ class FlowEngine:
         self._blocks = blocks
         for b in blocks:
             b.desc.range_flag = self.range_flag.data_ptr()
+        if FUSE_LEVELS is not None:
+            for l, L in enumerate(self.levels):
+                for b in self.couple[l] + [self.prior[l]]:
+                    b.desc.fuse_layers = 1 if L.h in FUSE_LEVELS else 0
         self.conv_mode = "dx3" if self.dx3 else ("x3" if self.wx3 else "f32")
         self.dxb = self.precision == "bf16" and DXB and any(b.dxb_w for b in blocks)
         if self.precision == "bf16":
@@ -329,6 +344,17 @@ class FlowEngine:
             return 0
         cm = self._dx3_cmax(l)
         return sum(1 for i in range(geom.depth) if cm is None or geom.k_in[i] <= cm)
+
+    def fused_block(self, l: int, blk) -> bool:
+        """Whether level l's block `blk` runs as one fused launch (IdfDenseBlock.fuse_layers):
+        every layer on dx3 / dxb at a geometry whose tiles hold whole images."""
+        d = blk.desc
+        if not d.fuse_layers or not (d.dx3 or d.dxb):
+            return False
+        if d.dx3 and self.dx3_layers(l, blk.geom) != blk.geom.depth:
+            return False
+        L = self.levels[l]
+        return bool(lib().idf_dx3_block_supported(L.h, L.w, blk.geom.g_pad, 1 if d.dxb else 0))
 
     def set_conv_mode(self, mode: str):
         """'dx3' (split-f16 direct conv where the geometry allows, split-f16 Winograd

@@ -29,6 +29,9 @@ VERSION = 2         # 2 adds the source (pre-pad) image size; version-1 streams 
 # header flags bit 0: the VQ decoder's 3x3 convs ran as split-f16 products (vq_conv "x3");
 # 0: exact-f32 Winograd (every stream written before the field existed)
 FLAG_VQ_X3 = 1
+# bit 1 (with bit 0): the other VQ convs ran as split-f16 products too (vq_conv "x3t",
+# idf_conv_taps_x3); absent in files written before round 6
+FLAG_VQ_TAPS = 2
 
 
 @dataclass
@@ -62,9 +65,9 @@ class ResidualBitstream:
     def to_bytes(self) -> bytes:
         C, H, W = self.image_shape
         sh, sw = self.source_hw or (H, W)
-        if self.vq_conv not in ("x3", "f32"):
+        if self.vq_conv not in ("x3t", "x3", "f32"):
             raise ValueError(f"unknown VQ conv mode {self.vq_conv!r}")
-        flags = FLAG_VQ_X3 if self.vq_conv == "x3" else 0
+        flags = {"x3t": FLAG_VQ_X3 | FLAG_VQ_TAPS, "x3": FLAG_VQ_X3, "f32": 0}[self.vq_conv]
         hdr = struct.pack("<4sHHIIIIIIIII", MAGIC, VERSION, flags, self.n_images, C, H, W,
                           self.grid[0], self.grid[1], self.embed_num, sh, sw)
         iw = self.idx_words.detach().cpu().numpy().astype("<i4").tobytes()
@@ -77,7 +80,7 @@ class ResidualBitstream:
         magic, ver, _f, n, C, H, W, h, w, K = struct.unpack_from(fmt, buf, 0)
         if magic != MAGIC or ver not in (1, VERSION):
             raise ValueError("not an IDF residual bitstream")
-        if _f & ~FLAG_VQ_X3:
+        if _f & ~(FLAG_VQ_X3 | FLAG_VQ_TAPS) or (_f & FLAG_VQ_TAPS and not _f & FLAG_VQ_X3):
             raise ValueError(f"unknown residual bitstream flags {_f:#x}")
         o = struct.calcsize(fmt)
         src = None
@@ -92,7 +95,7 @@ class ResidualBitstream:
         t = torch.from_numpy(iw)
         return cls(flow, t.to(device) if device else t, n, (C, H, W), (h, w), K,
                    None if src is None or tuple(src) == (H, W) else tuple(src),
-                   "x3" if _f & FLAG_VQ_X3 else "f32")
+                   "x3t" if _f & FLAG_VQ_TAPS else ("x3" if _f & FLAG_VQ_X3 else "f32"))
 
 
 class ResidualCodec:

@@ -105,6 +105,25 @@ def pack_convT(weight, bias) -> list[TapConv]:
     return out
 
 
+def taps_weights_x3(w: np.ndarray):
+    """Split-f16 form of a TapConv's W [n_alloc][ntaps][ldw] for idf_conv_taps_x3: W * 2^k (k:
+    packing.x3_scale, max |W| 2^k in [2^14, 2^15)) split wh = f16(w'), wl = f16(w' - wh) (both
+    round-to-nearest-even, from the fp32 weights widened to float64), laid out per 4 channels as
+    (wh[4], wl[4]) -- [n_alloc][ntaps][ldw / 4][8] uint16, the bytes of the fp32 array.  Returns
+    (that array, yscale = 2^-k)."""
+    from .packing import x3_scale
+    w64 = np.asarray(w, np.float64)
+    k = x3_scale(w64)
+    ws = w64 * (2.0 ** k)
+    hi = ws.astype(np.float16)
+    lo = (ws - hi.astype(np.float64)).astype(np.float16)
+    na, nt, ldw = w64.shape
+    out = np.empty((na, nt, ldw // 4, 8), np.uint16)
+    out[..., :4] = hi.view(np.uint16).reshape(na, nt, ldw // 4, 4)
+    out[..., 4:] = lo.view(np.uint16).reshape(na, nt, ldw // 4, 4)
+    return np.ascontiguousarray(out), float(2.0 ** -k)
+
+
 def _np(t):
     return t.detach().cpu().double().numpy()
 
@@ -194,18 +213,28 @@ class DevConv:
             self.wino_u = torch.from_numpy(wino_weights(c.w.astype(np.float64), nslab, U)).to(device)
             ux3, self.wx3_yscale = wino_weights_x3(c.w.astype(np.float64), nslab, U)
             self.wx3_u = torch.from_numpy(ux3.view(np.int16)).to(device)
+        # the tap GEMM's split-f16 weights (VQ conv mode "x3t", idf_conv_taps_x3)
+        self.wt_x3 = None
+        self.wt_yscale = 1.0
+        if wino and self.wino_u is None:
+            wt, self.wt_yscale = taps_weights_x3(c.w)
+            self.wt_x3 = torch.from_numpy(wt.view(np.int16)).to(device)
         self.b = torch.from_numpy(c.bias).to(device)
         self.dy = (ctypes.c_int32 * len(c.dy))(*c.dy)
         self.dx = (ctypes.c_int32 * len(c.dx))(*c.dx)
 
 
-VQ_CONV_MODES = ("x3", "f32")
+# "x3t": ResBlock 3x3 convs on split-f16 Winograd (wx3) and every other conv on the split-f16
+# tap GEMM (idf_conv_taps_x3); "x3": round 3-5's -- wx3 ResBlocks, the other convs in exact fp32;
+# "f32": everything exact fp32.  The decoder runs the mode its bitstream records.
+VQ_CONV_MODES = ("x3t", "x3", "f32")
+SPLIT_VQ = ("x3t", "x3")
 
 
 class VQEngine:
     """Device VQ-VAE: indices and reconstruction of a batch of images.
 
-    conv_mode ("x3" default, IDF_VQ_CONV overrides): the arithmetic of the 3x3 ResBlock convs.
+    conv_mode ("x3t" default, IDF_VQ_CONV overrides; VQ_CONV_MODES): the arithmetic of the convs.
     encode_pm / decode_pm run it and fall back to "f32" for the whole pass when the split-f16
     range guard trips; last_decode_mode is the mode the last decode_pm ran (what the encoder
     records for its receiver)."""
@@ -214,7 +243,7 @@ class VQEngine:
         import os
         self.device = device
         self.wino = wino
-        self.conv_mode = os.environ.get("IDF_VQ_CONV", "x3") if wino else "f32"
+        self.conv_mode = os.environ.get("IDF_VQ_CONV", "x3t") if wino else "f32"
         if self.conv_mode not in VQ_CONV_MODES:
             raise ValueError(f"IDF_VQ_CONV={self.conv_mode!r}: one of {VQ_CONV_MODES}")
         self.last_decode_mode = self.conv_mode
@@ -256,7 +285,10 @@ class VQEngine:
             # priced as the direct conv it computes; a transposed conv's launch covers one output
             # parity: its taps on the input grid)
             grid = B * (H * W if (dc.wino_u is not None or c.osy == 2) else Ho * Wo)
-            kind = ("resblock3x3_" + self._mode) if dc.wino_u is not None else "conv_taps"
+            split = self._mode in SPLIT_VQ
+            kind = (("resblock3x3_x3" if split else "resblock3x3_f32") if dc.wino_u is not None
+                    else ("conv_taps_x3" if self._mode == "x3t" and dc.wt_x3 is not None
+                          else "conv_taps"))
             t0, t1 = self._timed(kind, 2.0 * grid * len(c.dy) * c.cin * c.cout)
         else:
             t0 = t1 = lambda: None
@@ -271,7 +303,7 @@ class VQEngine:
             L = lib()
             wsn = int(L.idf_conv3x3_wino_workspace(B, H, W, c.cin, c.cout))
             ws = self._wino_ws(wsn)
-            if self._mode == "x3":
+            if self._mode in SPLIT_VQ:
                 check(L.idf_conv3x3_wx3_res(
                     s, B, H, W, c.cin, ptr(x), ldx, ptr(dc.wx3_u), c.n_alloc // 16,
                     dc.wx3_yscale, ptr(dc.b), c.cout, ptr(out), ldo,
@@ -287,6 +319,13 @@ class VQEngine:
             Hc, Wc = H, W
         else:
             Hc, Wc = Ho, Wo
+        if self._mode == "x3t" and dc.wt_x3 is not None:
+            check(lib().idf_conv_taps_x3(
+                s, B, H, W, round_up(c.cin, 4), ptr(x), ldx, Hc, Wc, c.isy, c.isy, len(c.dy), dc.dy,
+                dc.dx, ptr(dc.wt_x3), c.ldw, c.n_alloc, dc.wt_yscale, ptr(dc.b), c.cout, ptr(out),
+                ldo, Ho, Wo, c.osy, c.osy, c.oy0, c.ox0, ptr(res) if res is not None else None, ldr,
+                act, LEAKY, ptr(self.flag)), "vq conv x3t")
+            return
         check(lib().idf_conv_taps_f32(
             s, B, H, W, round_up(c.cin, 4), ptr(x), ldx, Hc, Wc, c.isy, c.isy, len(c.dy), dc.dy,
             dc.dx, ptr(dc.w), c.ldw, c.n_alloc, ptr(dc.b), c.cout, ptr(out), ldo, Ho, Wo, c.osy,
@@ -304,11 +343,11 @@ class VQEngine:
         mode = mode or self.conv_mode
         if mode not in VQ_CONV_MODES:
             raise ValueError(f"unknown VQ conv mode {mode!r}")
-        if mode == "x3":
+        if mode in SPLIT_VQ:
             self.flag.zero_()
         self._mode = mode
         out = self._run(stages, x, B, H, W, C)
-        if mode == "x3" and bool(self.flag.item()):
+        if mode in SPLIT_VQ and bool(self.flag.item()):
             self._mode = mode = "f32"
             out = self._run(stages, x, B, H, W, C)
         self._mode = self.conv_mode

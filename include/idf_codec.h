@@ -219,6 +219,12 @@ typedef struct IdfDenseBlock {
    * of idf_conv3x3_bf16 -- another sum order, so it is part of the conv arithmetic too */
   int32_t dxb;
   const uint16_t *dxb_w[IDF_MAX_DEPTH];
+  /* fuse_layers = 1: a block whose layers all run on dx3 / dxb, at a geometry whose tiles hold
+   * whole images (16-wide images of <= 16 rows, the 4- and 8-wide packed images), runs every
+   * layer in ONE launch, one workgroup per tile (conv3_dx3_block_kernel), the fused head's sums
+   * in registers.  An execution choice only: outputs, split copy, head results and range flag
+   * are bit for bit those of the per-layer launches (not recorded in a bitstream). */
+  int32_t fuse_layers;
 } IdfDenseBlock;
 
 /* Head epilogue target */
@@ -250,6 +256,10 @@ typedef struct IdfHeadOut {
 int idf_dense_block_f32(void *stream, const IdfDenseBlock *blk, int32_t B, int32_t H, int32_t W,
                         float *d_feat, int64_t ld_feat, float *d_tmp, int64_t ld_tmp,
                         const IdfHeadOut *head);
+/* 1 when a DenseBlock of growth N on dx3 (bf = 0) or dxb (bf = 1) at H x W runs as one fused
+ * launch (IdfDenseBlock.fuse_layers): the tiles hold whole images. */
+int idf_dx3_block_supported(int32_t H, int32_t W, int32_t N, int32_t bf);
+
 /* Bytes of tmp the block's direct-conv layers and fused head need at B images of HxW (0: the
  * block runs no dx3 / dxb layer there; -1: bad arguments).  A function of the block and the
  * geometry only. */
@@ -518,6 +528,20 @@ int idf_conv_taps_f32(void *stream, int32_t B, int32_t Hi, int32_t Wi, int32_t C
                       int32_t n_alloc, const float *d_bias, int32_t N, float *d_out, int64_t ld_out,
                       int32_t Ho, int32_t Wo, int32_t osy, int32_t osx, int32_t oy0, int32_t ox0,
                       const float *d_res, int64_t ld_res, int32_t act, float slope);
+/* The same convolution with split-f16 products (VQ conv mode "x3t"): d_w holds, per 16 bytes,
+ * (wh[4], wl[4]) f16 of 4 consecutive channels of W * 2^k (wh = f16(w'), wl = f16(w' - wh),
+ * split on the host, vq.py taps_weights_x3) in W's [n_alloc][ntaps][ldw] order, yscale = 2^-k;
+ * every input value x = xh + xl is split when its tile is staged and each product taken as
+ * xh.wh + xl.wh + xh.wl on v_mfma_f32_16x16x16_f16 with fp32 accumulation (the flow's dx3 /
+ * wx3 arithmetic).  A NaN or |x| >= 32768 among the inputs ORs bit 0 into *d_flag (NULL: not
+ * checked): the caller recomputes with idf_conv_taps_f32. */
+int idf_conv_taps_x3(void *stream, int32_t B, int32_t Hi, int32_t Wi, int32_t C, const float *d_x,
+                     int64_t ld_x, int32_t Hc, int32_t Wc, int32_t isy, int32_t isx, int32_t ntaps,
+                     const int32_t *dy, const int32_t *dx, const uint16_t *d_w, int32_t ldw,
+                     int32_t n_alloc, float yscale, const float *d_bias, int32_t N, float *d_out,
+                     int64_t ld_out, int32_t Ho, int32_t Wo, int32_t osy, int32_t osx, int32_t oy0,
+                     int32_t ox0, const float *d_res, int64_t ld_res, int32_t act, float slope,
+                     uint32_t *d_flag);
 /* VectorQuantizer.forward's index (roundlib.py:56-62): enorm[k] = |e_k|^2, then
  * idx[p] = argmin_k ((|x_p|^2 + enorm[k]) - 2 x_p.e_k), lowest k on ties; D, ld_x, lde
  * multiples of 4.  With a device workspace of idf_vq_argmin_workspace_bytes(P, K) bytes the

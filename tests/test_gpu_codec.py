@@ -162,16 +162,29 @@ def test_range_guard_clean_on_real_batch():
     assert bs.meta["conv"] == "dx3" and not eng.range_flag_tripped()
 
 
-def test_round4_code6_bitstream_decodes_exactly(golden):
-    """A conv-code-6 bitstream written by the round-4 build itself (tests/golden/
-    imagenet64_code6_r4.npz, from make_code6_fixture.py at 23b932c: round 4's dx3 at the 16-wide
-    levels) decodes with today's library to the exact images: code 6 ("dx3w16") still names the
+@pytest.mark.parametrize("fixture,conv", [("imagenet64_code6_r4.npz", "dx3w16"),
+                                          ("imagenet64_code7_r5.npz", "dx3"),
+                                          ("config3_code8_r5.npz", "dxb")])
+def test_earlier_build_bitstreams_decode_exactly(golden, fixture, conv):
+    """Bitstreams written by earlier builds themselves (tests/golden/make_conv_fixture.py): conv
+    code 6 at 23b932c (round 4's dx3 at the 16-wide levels, read today as "dx3w16"), code 7 and
+    code 8 at 92c5486 (round 5's dx3 and dxb, the latter inside a config-3 residual bitstream)
+    decode with today's library to the exact images: each recorded conv code still names the
     arithmetic it was written with, bit for bit."""
+    from idfcodec import configs, synthetic
     from idfcodec.codec import Bitstream
-    d = golden("imagenet64_code6_r4.npz")
-    bs = Bitstream.from_bytes(d["bitstream"].tobytes())
-    assert bs.meta["conv"] == "dx3w16"
-    model = _imagenet64()
-    out, info = model.codec().decode(bs)
+    from idfcodec.residual import ResidualBitstream
+    d = golden(fixture)
+    raw = d["bitstream"].tobytes()
+    if fixture.startswith("imagenet64"):
+        bs = Bitstream.from_bytes(raw)
+        assert bs.meta["conv"] == conv
+        out, info = _imagenet64().codec().decode(bs)
+    else:
+        name = str(d["config"])
+        rbs = ResidualBitstream.from_bytes(raw)
+        assert rbs.flow.meta["conv"] == conv
+        codec, _, _, _ = synthetic.build_residual(name)
+        out, info = codec.decode(rbs)
     assert info["ok"], info
-    assert torch.equal(out.cpu(), torch.from_numpy(d["images"])), "round-4 file decodes wrong"
+    assert torch.equal(out.cpu(), torch.from_numpy(d["images"])), "an earlier file decodes wrong"

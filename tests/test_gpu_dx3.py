@@ -490,3 +490,53 @@ def test_dx3_split_copy_over_2gib():
         one = run(X[i * hw:(i + 1) * hw].contiguous(), 1)
         assert torch.equal(full[i * hw:(i + 1) * hw], one), i
     assert full.abs().sum() > 0
+
+
+@pytest.mark.parametrize("name,lvl,which", [
+    ("imagenet64", 1, "coupling"), ("imagenet64", 1, "prior"),
+    ("resflows_smallpatch_split", 0, "coupling"), ("resflow-cond-imagenet64", 1, "coupling"),
+    ("resflow-cond-imagenet64", 1, "prior")])
+def test_fused_block_kernel_bit_identical(name, lvl, which):
+    """The fused DenseBlock launch (IdfDenseBlock.fuse_layers: every layer in one launch, one
+    workgroup per tile, conv3_dx3_block_kernel) gives the per-layer launches' bits: the head's
+    outputs (fused head: its register sums and epilogue; GEMM head: over the fp32 features the
+    layers stored) and the fp32 features.  imagenet64's 16x16 level, config 4's 4x4 patches,
+    config 3's bf16 (dxb) blocks."""
+    from idfcodec import _lib, configs, synthetic
+    from idfcodec._lib import IdfHeadOut, ptr
+    model = synthetic.build_model(configs.get(name)).cuda()
+    model.idf_precision = configs.PRECISION.get(name, "f32")
+    eng = model.engine()
+    Lv = eng.levels[lvl]
+    blk = eng.couple[lvl][0] if which == "coupling" else eng.prior[lvl]
+    bf = 1 if blk.desc.dxb else 0
+    assert blk.desc.dx3 == 1 or blk.desc.dxb == 1
+    assert _lib.lib().idf_dx3_block_supported(Lv.h, Lv.w, blk.geom.g_pad, bf) == 1
+    B = 48 if Lv.h * Lv.w >= 64 else 200
+    P = B * Lv.h * Lv.w
+    k0 = blk.geom.k_in[0]
+    nh = blk.geom.n_head
+    ldo = (nh + 3) // 4 * 4
+    g = torch.Generator().manual_seed(11)
+    x = (torch.randint(-64, 64, (P, k0), generator=g).float() / 256).cuda()
+    if which == "coupling":
+        x[:, Lv.a:] = 0.0
+    ws = eng.workspace(B, 1)
+    res = []
+    for fuse in (0, 1):
+        blk.desc.fuse_layers = fuse
+        feat = ws["feat"].view(-1, eng.ld_feat)
+        feat.zero_()
+        feat[:P, :k0] = x
+        out = torch.zeros(P, ldo, device="cuda")
+        h = IdfHeadOut()
+        h.mode, h.out, h.ld_out = _lib.EPI_STORE, ptr(out), ldo
+        blk.run(_lib.stream_ptr(), B, Lv.h, Lv.w, ptr(ws["feat"]), eng.ld_feat, ptr(ws["tmp"]),
+                eng.tmp_pitch(ws, P), h)
+        torch.cuda.synchronize()
+        res.append((out.clone(), feat[:P, :blk.geom.k_in[-1]].clone()))
+    blk.desc.fuse_layers = 1
+    (o0, f0), (o1, f1) = res
+    assert torch.isfinite(o0).all() and o0.abs().sum() > 0
+    assert torch.equal(o0, o1), int((o0 != o1).any(1).sum())
+    assert torch.equal(f0, f1), int((f0 != f1).any(1).sum())

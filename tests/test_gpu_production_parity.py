@@ -357,7 +357,7 @@ def test_config45_full_size_streams_vs_oracle(oracle, name, src, B):
     codec, fl, vq, size = synthetic.build_residual(name)
     x = synthetic.images(B, H=src[0], W=src[1], seed=23).cuda()
     rbs = codec.encode(x)
-    assert rbs.vq_conv == "x3" and rbs.flow.meta.get("conv") == "dx3"
+    assert rbs.vq_conv == "x3t" and rbs.flow.meta.get("conv") == "dx3"
     n = _sampled_streams_vs_oracle(oracle, fl, rbs, seed=len(name))
     assert n >= 10
     out, info = codec.decode(rbs)

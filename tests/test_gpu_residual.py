@@ -46,24 +46,26 @@ def test_residual_round_trip_small(kind, img, patch):
     codec = ResidualCodec(fl, vq, (H, W))
     x = synthetic.images(3, H=H, W=W, seed=21).cuda()
     rbs = codec.encode(x)
-    assert rbs.vq_conv == "x3"  # the VQ ResBlock convs ran split-f16, guard not tripped
+    assert rbs.vq_conv == "x3t"  # every VQ conv ran split-f16, guard not tripped
     raw = rbs.to_bytes()
     rbs2 = ResidualBitstream.from_bytes(raw, device="cuda")
-    assert rbs2.vq_conv == "x3"
+    assert rbs2.vq_conv == "x3t"
     out, info = codec.decode(rbs2)
     assert info["ok"], info
     assert torch.equal(out, x)
     assert rbs.bits() > 0 and rbs.index_bits == 6
-    # an exact-f32 VQ encode is recorded as such and decodes exactly on the same engine
+    # an "x3" (round 5's: split-f16 ResBlocks only) or exact-f32 VQ encode is recorded as such
+    # and decodes exactly on the same engine
     eng = vq.engine()
-    eng.conv_mode = "f32"
-    try:
-        r32 = codec.encode(x)
-    finally:
-        eng.conv_mode = "x3"
-    assert r32.vq_conv == "f32"
-    out, info = codec.decode(ResidualBitstream.from_bytes(r32.to_bytes(), device="cuda"))
-    assert info["ok"] and torch.equal(out, x)
+    for mode in ("x3", "f32"):
+        eng.conv_mode = mode
+        try:
+            r32 = codec.encode(x)
+        finally:
+            eng.conv_mode = "x3t"
+        assert r32.vq_conv == mode
+        out, info = codec.decode(ResidualBitstream.from_bytes(r32.to_bytes(), device="cuda"))
+        assert info["ok"] and torch.equal(out, x)
 
 
 def test_config3_round_trip():

@@ -39,11 +39,12 @@ def model_for(name):
     return m.cuda().eval(), z
 
 
-@pytest.mark.parametrize("mode", ["x3", "f32"])
+@pytest.mark.parametrize("mode", ["x3t", "x3", "f32"])
 @pytest.mark.parametrize("name", list(CASES))
 def test_vqvae_engine_matches_reference(name, mode):
-    """Both conv modes of the ResBlock 3x3 convs: split-f16 products (the default) and the
-    exact-f32 Winograd kernel; neither's range guard trips on the reference's data."""
+    """The three VQ conv modes: every conv on split-f16 products ("x3t", the default), the
+    ResBlock 3x3 convs only ("x3", round 5's) and exact f32; no range guard trips on the
+    reference's data."""
     m, z = model_for(name)
     m.engine().conv_mode = mode
     data = torch.from_numpy(z["data"]).cuda()
@@ -80,7 +81,7 @@ def test_vq_range_guard_falls_back_to_f32():
     mode exactly (what a decoder does with the bitstream's vq_conv)."""
     m, z = model_for("vq_t2_2down")
     eng = m.engine()
-    eng.conv_mode = "x3"
+    eng.conv_mode = "x3t"
     B, D = 2, m.embed_dim
     from idfcodec.packing import round_up
     g = torch.Generator().manual_seed(3)
@@ -93,7 +94,7 @@ def test_vq_range_guard_falls_back_to_f32():
     y32, *_, mode32 = eng._guarded(eng.dec, big, B, h, w, D, mode="f32")
     assert mode32 == "f32" and torch.equal(y, y32)
     ridx = torch.from_numpy(z["idx"]).cuda()
-    for mode in ("x3", "f32"):
+    for mode in ("x3t", "x3", "f32"):
         a = m.reconstruct(ridx, conv=mode)
         assert eng.last_decode_mode == mode
         assert torch.equal(a, m.reconstruct(ridx, conv=mode))
@@ -162,3 +163,75 @@ def test_vq_argmin_slices_equal_one_pass(P, K, D):
         assert ok.float().mean() > 0.3
         assert torch.equal(one.cpu().long()[ok], order[ok, 0])
     assert not (one.cpu() == K // 2).any()  # the duplicate of code K // 3 never wins
+
+
+@pytest.mark.parametrize("kind,ci,co,H,W", [("conv4s2", 3, 128, 64, 64), ("conv4s2", 128, 256, 32, 32),
+                                            ("conv3", 40, 24, 9, 7), ("conv1", 384, 512, 8, 8),
+                                            ("convT", 384, 256, 8, 8), ("convT", 256, 3, 16, 16)])
+def test_conv_taps_x3_vs_fp64(kind, ci, co, H, W):
+    """idf_conv_taps_x3 (split-f16 products on f16 MFMA) against a float64 conv of the same
+    fp32 inputs and weights: within 1e-5 of the output scale and at most 4x the exact-f32
+    kernel's own error; the strided, 3x3, 1x1 and transposed (four parity launches) forms; an
+    input past the f16 pairs' range sets the flag."""
+    import torch.nn.functional as F
+    from idfcodec import _lib, vq
+    from idfcodec._lib import check, ptr
+    from idfcodec.packing import round_up
+    g = torch.Generator().manual_seed(ci * 7 + co)
+    B = 3
+    x = torch.randn(B, ci, H, W, generator=g, dtype=torch.float64)
+    x32 = x.float()  # the kernels see fp32 operands; so does the float64 reference
+    if kind == "convT":
+        w = (torch.randn(ci, co, 4, 4, generator=g, dtype=torch.float64) * 0.05).float()
+        ref = F.conv_transpose2d(x32.double(), w.double(), stride=2, padding=1)
+        convs = vq.pack_convT(w.double().numpy(), None)
+    else:
+        k, st, pd = {"conv4s2": (4, 2, 1), "conv3": (3, 1, 1), "conv1": (1, 1, 0)}[kind]
+        w = (torch.randn(co, ci, k, k, generator=g, dtype=torch.float64) * 0.05).float()
+        ref = F.conv2d(x32.double(), w.double(), stride=st, padding=pd)
+        convs = [vq.pack_conv(w.double().numpy(), None, stride=st, padding=pd)]
+    Ho, Wo = ref.shape[2], ref.shape[3]
+    ldx = round_up(ci, 4)
+    xp = torch.zeros(B, H, W, ldx)
+    xp[..., :ci] = x32.permute(0, 2, 3, 1)
+    xp = xp.cuda().contiguous()
+    ldo = round_up(co, 4)
+    L = _lib.lib()
+    outs = {}
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    for mode in ("x3", "f32"):
+        out = torch.zeros(B * Ho * Wo * ldo, device="cuda")
+        for c in convs:
+            dc = vq.DevConv(c, "cuda", wino=False)  # the fp32 tap weights and bias
+            wt, ys = vq.taps_weights_x3(c.w)        # (a 3x3 conv's engine path is Winograd)
+            wt = torch.from_numpy(wt.view(np.int16)).cuda()
+            Hc, Wc = (H, W) if c.osy == 2 else (Ho, Wo)
+            args = (_lib.stream_ptr(), B, H, W, ldx, ptr(xp), ldx, Hc, Wc, c.isy, c.isy, len(c.dy),
+                    dc.dy, dc.dx)
+            tail = (ptr(out), ldo, Ho, Wo, c.osy, c.osy, c.oy0, c.ox0, None, 0, 3, 0.0)
+            if mode == "x3":
+                check(L.idf_conv_taps_x3(*args, ptr(wt), c.ldw, c.n_alloc, ys, ptr(dc.b), co,
+                                         *tail, ptr(flag)), "taps x3")
+            else:
+                check(L.idf_conv_taps_f32(*args, ptr(dc.w), c.ldw, c.n_alloc, ptr(dc.b), co, *tail),
+                      "taps f32")
+        outs[mode] = out.view(B, Ho, Wo, ldo)[..., :co].permute(0, 3, 1, 2).double().cpu()
+    assert int(flag.item()) == 0
+    scale = ref.abs().max().item()
+    e3 = (outs["x3"] - ref).abs().max().item() / scale
+    e32 = (outs["f32"] - ref).abs().max().item() / scale
+    print(f"{kind} {ci}->{co}: split-f16 {e3:.2e}, f32 {e32:.2e}")
+    assert e3 < 1e-5 and e3 <= 4 * e32 + 1e-7, (e3, e32)
+    # past the f16 pairs' range: flagged
+    xp[0, 0, 0, 0] = 1e5
+    c = convs[0]
+    dc = vq.DevConv(c, "cuda", wino=False)
+    wt, ys = vq.taps_weights_x3(c.w)
+    wt = torch.from_numpy(wt.view(np.int16)).cuda()
+    Hc, Wc = (H, W) if c.osy == 2 else (Ho, Wo)
+    out = torch.zeros(B * Ho * Wo * ldo, device="cuda")
+    check(L.idf_conv_taps_x3(_lib.stream_ptr(), B, H, W, ldx, ptr(xp), ldx, Hc, Wc, c.isy, c.isy,
+                             len(c.dy), dc.dy, dc.dx, ptr(wt), c.ldw, c.n_alloc,
+                             ys, ptr(dc.b), co, ptr(out), ldo, Ho, Wo, c.osy, c.osy,
+                             c.oy0, c.ox0, None, 0, 3, 0.0, ptr(flag)), "taps x3")
+    assert int(flag.item()) == 1

@@ -279,8 +279,12 @@ def test_residual_container_roundtrip_and_source_size():
     x3 = ResidualBitstream(flow, idx, 1, (3, 216, 184), (27, 23), 8192, None, "x3").to_bytes()
     assert struct.unpack_from("<H", x3, 6)[0] == 1
     assert ResidualBitstream.from_bytes(x3).vq_conv == "x3"
-    with pytest.raises(ValueError, match="flags"):
-        ResidualBitstream.from_bytes(x3[:6] + struct.pack("<H", 6) + x3[8:])
+    x3t = ResidualBitstream(flow, idx, 1, (3, 216, 184), (27, 23), 8192, None, "x3t").to_bytes()
+    assert struct.unpack_from("<H", x3t, 6)[0] == 3
+    assert ResidualBitstream.from_bytes(x3t).vq_conv == "x3t"
+    for bad in (6, 2):  # an unknown bit; the taps bit without the ResBlocks' bit
+        with pytest.raises(ValueError, match="flags"):
+            ResidualBitstream.from_bytes(x3[:6] + struct.pack("<H", bad) + x3[8:])
 
 
 # ------------------------------------------------------------------ coder chaining (F4)
@@ -483,11 +487,27 @@ def test_decode_rejects_mismatched_container():
         Bitstream.from_bytes(bytes(bad))
 
 
-def test_round4_code6_fixture_header(golden):
-    """The round-4 fixture (tests/golden/make_code6_fixture.py at 23b932c) is a version-2 container
-    with conv code 6, which reads as "dx3w16"; its decode is tests/test_gpu_codec.py's."""
+def test_earlier_build_fixture_headers(golden):
+    """The earlier builds' fixtures (tests/golden/make_conv_fixture.py) read with their conv codes
+    -- 6 ("dx3w16"), 7 ("dx3") -- and re-serialise byte for byte; their decodes are
+    tests/test_gpu_codec.py's."""
     from idfcodec.codec import Bitstream
-    d = golden("imagenet64_code6_r4.npz")
-    bs = Bitstream.from_bytes(d["bitstream"].tobytes())
-    assert bs.meta["conv"] == "dx3w16" and bs.n_images == d["images"].shape[0] == 4
-    assert bs.to_bytes() == d["bitstream"].tobytes()  # re-serialises byte for byte
+    for name, conv in (("imagenet64_code6_r4.npz", "dx3w16"), ("imagenet64_code7_r5.npz", "dx3")):
+        d = golden(name)
+        bs = Bitstream.from_bytes(d["bitstream"].tobytes())
+        assert bs.meta["conv"] == conv and bs.n_images == d["images"].shape[0] == 4
+        assert bs.to_bytes() == d["bitstream"].tobytes()  # re-serialises byte for byte
+
+
+def test_fused_block_geometries():
+    """The fused DenseBlock launch (idf_dx3_block_supported) takes exactly the geometries whose
+    tiles hold whole images, with one output group and no split K: 16x16 and the packed 4x4
+    images -- not 8x8 (split K: the per-layer launches are faster), 32x32 (four tiles an
+    image), 27x23 or 2x2 (gutter bands crossing tiles), nor 128 outputs (two output groups)."""
+    from idfcodec import _lib
+    sup = _lib.lib().idf_dx3_block_supported
+    for (H, W, N, bf), want in [((16, 16, 48, 0), 1), ((8, 8, 48, 0), 0), ((4, 4, 32, 0), 1),
+                                ((16, 16, 48, 1), 1), ((8, 8, 48, 1), 0), ((32, 32, 48, 0), 0),
+                                ((27, 23, 32, 0), 0), ((2, 2, 32, 0), 0), ((4, 4, 128, 0), 0),
+                                ((64, 64, 48, 0), 0)]:
+        assert sup(H, W, N, bf) == want, (H, W, N, bf)
