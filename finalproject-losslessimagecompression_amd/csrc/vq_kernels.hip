@@ -266,6 +266,11 @@ __device__ __forceinline__ bool vq_better(float d, int k, float bd, int bk) {
   return d < bd || (d == bd && k < bk);  // NaN never wins
 }
 
+// X3 = true: x.e with split-f16 products (xh.eh + xl.eh + xh.el on v_mfma_f32_16x16x16_f16, fp32
+// accumulation; E pre-split on the host as (eh[4], el[4]) per 4 channels of E * 2^k, yscale =
+// 2^-k), |x|^2 and |e|^2 still fp32 in index order; an input value past the f16 pairs' range
+// (NaN or |x| >= 32768) ORs bit 0 into flag (the caller searches again in fp32).
+template <bool X3>
 __global__ void __launch_bounds__(256) vq_argmin_kernel(int64_t P, int32_t D, const float* __restrict__ X,
                                                         int64_t ldx, const float* __restrict__ E,
                                                         int32_t lde, int32_t K,
@@ -273,7 +278,8 @@ __global__ void __launch_bounds__(256) vq_argmin_kernel(int64_t P, int32_t D, co
                                                         int32_t slice_codes,
                                                         float* __restrict__ part_d,
                                                         int32_t* __restrict__ part_i,
-                                                        int32_t* __restrict__ idx) {
+                                                        int32_t* __restrict__ idx, float yscale,
+                                                        uint32_t* __restrict__ flag) {
   __shared__ __attribute__((aligned(16))) float As[2][kVqBM][kVqPitch];
   __shared__ __attribute__((aligned(16))) float Bs[2][kVqBN][kVqPitch];
   __shared__ float x2s[kVqBM];
@@ -299,8 +305,18 @@ __global__ void __launch_bounds__(256) vq_argmin_kernel(int64_t P, int32_t D, co
     rb0 = (n0 < ke && c < D) ? *(const f4*)(E + (int64_t)n0 * lde + c) : f4{0.f, 0.f, 0.f, 0.f};
     rb1 = (n1 < ke && c < D) ? *(const f4*)(E + (int64_t)n1 * lde + c) : f4{0.f, 0.f, 0.f, 0.f};
   };
+  bool in_ok = true;
   auto store = [&](int buf) {
-    *(f4*)&As[buf][ar][aq] = ra;
+    if constexpr (X3) {  // (xh[4], xl[4]) in the 16 bytes of the 4 fp32 values
+      typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+      in_ok = in_ok && fabsf(ra[0]) < 32768.0f && fabsf(ra[1]) < 32768.0f &&
+              fabsf(ra[2]) < 32768.0f && fabsf(ra[3]) < 32768.0f;
+      const h4 hi = __builtin_convertvector(ra, h4);
+      const h4 lo = __builtin_convertvector(ra - __builtin_convertvector(hi, f4), h4);
+      *(h8*)&As[buf][ar][aq] = h8{hi[0], hi[1], hi[2], hi[3], lo[0], lo[1], lo[2], lo[3]};
+    } else {
+      *(f4*)&As[buf][ar][aq] = ra;
+    }
     *(f4*)&Bs[buf][ar][aq] = rb0;
     *(f4*)&Bs[buf][64 + ar][aq] = rb1;
   };
@@ -315,6 +331,12 @@ __global__ void __launch_bounds__(256) vq_argmin_kernel(int64_t P, int32_t D, co
     }
   float x2acc = 0.0f;  // thread tid < 64: |x_row|^2 in index order, formed on the first tile
   bool first = true;
+  if constexpr (X3) {  // (the staged tile holds halves): from the rows themselves, same order
+    if (tid < kVqBM && m0 + tid < P) {
+      const float* xr = X + (m0 + tid) * ldx;
+      for (int c = 0; c < D; ++c) x2acc = __builtin_fmaf(xr[c], xr[c], x2acc);
+    }
+  }
   for (int k0 = kb; k0 < ke; k0 += kVqBN) {
     f4 acc[2][4];
 #pragma unroll
@@ -332,17 +354,34 @@ __global__ void __launch_bounds__(256) vq_argmin_kernel(int64_t P, int32_t D, co
       for (int i = 0; i < 2; ++i) fa[i] = *(const f4*)&As[buf][wr * 32 + i * 16 + lr][lk];
 #pragma unroll
       for (int j = 0; j < 4; ++j) fb[j] = *(const f4*)&Bs[buf][wc * 64 + j * 16 + lr][lk];
-      if (first && tid < kVqBM) {
+      if (!X3 && first && tid < kVqBM) {
         const int cn = D - kc * kVqBK < kVqBK ? D - kc * kVqBK : kVqBK;
         for (int c = 0; c < cn; ++c) x2acc = __builtin_fmaf(As[buf][tid][c], As[buf][tid][c], x2acc);
       }
+      if constexpr (X3) {
+        typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+        for (int i = 0; i < 2; ++i) {
+          const h8 a8 = __builtin_bit_cast(h8, fa[i]);
+          const h4 ah = h4{a8[0], a8[1], a8[2], a8[3]}, al = h4{a8[4], a8[5], a8[6], a8[7]};
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+          for (int j = 0; j < 4; ++j) {
+            const h8 b8 = __builtin_bit_cast(h8, fb[j]);
+            const h4 bh = h4{b8[0], b8[1], b8[2], b8[3]}, bl = h4{b8[4], b8[5], b8[6], b8[7]};
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bh, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x16f16(al, bh, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bl, acc[i][j], 0, 0, 0);
+          }
+        }
+      } else {
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][t], fb[j][t], acc[i][j], 0, 0, 0);
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][t], fb[j][t], acc[i][j], 0, 0, 0);
+      }
       if (kc + 1 < nkc) store(buf ^ 1);
       __syncthreads();
     }
@@ -362,7 +401,7 @@ __global__ void __launch_bounds__(256) vq_argmin_kernel(int64_t P, int32_t D, co
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float x2 = x2s[wr * 32 + i * 16 + (lane >> 4) * 4 + r];
-          const float d = (x2 + en) - 2.0f * acc[i][j][r];
+          const float d = (x2 + en) - 2.0f * (X3 ? acc[i][j][r] * yscale : acc[i][j][r]);
           if (vq_better(d, k, best[i][r], bidx[i][r])) {
             best[i][r] = d;
             bidx[i][r] = k;
@@ -370,6 +409,7 @@ __global__ void __launch_bounds__(256) vq_argmin_kernel(int64_t P, int32_t D, co
         }
     }
   }
+  if (X3 && !in_ok && flag) atomicOr(flag, 1u);
   // reduce over the 16 lanes sharing each row (lanes differ in code column), then the two
   // waves sharing each row (code halves)
 #pragma unroll
@@ -636,11 +676,12 @@ int64_t idf_vq_argmin_workspace_bytes(int64_t P, int32_t K) {
   return S > 1 ? (int64_t)S * P * 8 : 0;
 }
 
-int idf_vq_argmin_ws(void* stream, int64_t P, int32_t D, const float* x, int64_t ld_x, const float* e,
-                     int32_t lde, int32_t K, const float* enorm, int32_t* idx, void* ws,
-                     int64_t ws_bytes) {
+static int vq_argmin_run(bool x3, void* stream, int64_t P, int32_t D, const float* x, int64_t ld_x,
+                         const float* e, int32_t lde, int32_t K, const float* enorm, int32_t* idx,
+                         void* ws, int64_t ws_bytes, float yscale, uint32_t* d_flag) {
   if (P <= 0) return IDF_OK;
-  if (D <= 0 || (D & 3) || (ld_x & 3) || (lde & 3) || K <= 0) return IDF_ERR_ARG;
+  if (D <= 0 || (D & 3) || (ld_x & 3) || (lde & 3) || K <= 0 || !x || !e || !enorm || !idx)
+    return IDF_ERR_ARG;
   int S = vq_slices(P, K);
   if (!ws || ws_bytes < (int64_t)S * P * 8) S = 1;  // no room for the slices' minima
   // codes per slice, whole code tiles (the last slice may be short or empty)
@@ -648,12 +689,30 @@ int idf_vq_argmin_ws(void* stream, int64_t P, int32_t D, const float* x, int64_t
   float* pd = (float*)ws;
   int32_t* pi = (int32_t*)(pd + (S > 1 ? (int64_t)S * P : 0));
   const int64_t blocks = (P + kVqBM - 1) / kVqBM * S;
-  hipLaunchKernelGGL(vq_argmin_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, P, D,
-                     x, ld_x, e, lde, K, enorm, S, sc, pd, pi, idx);
+  if (x3)
+    hipLaunchKernelGGL(vq_argmin_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                       P, D, x, ld_x, e, lde, K, enorm, S, sc, pd, pi, idx, yscale, d_flag);
+  else
+    hipLaunchKernelGGL(vq_argmin_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                       P, D, x, ld_x, e, lde, K, enorm, S, sc, pd, pi, idx, 1.0f, nullptr);
   if (S > 1)
     hipLaunchKernelGGL(vq_argmin_merge_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, P, S, pd, pi, idx);
   return idf_last_error();
+}
+
+int idf_vq_argmin_ws(void* stream, int64_t P, int32_t D, const float* x, int64_t ld_x, const float* e,
+                     int32_t lde, int32_t K, const float* enorm, int32_t* idx, void* ws,
+                     int64_t ws_bytes) {
+  return vq_argmin_run(false, stream, P, D, x, ld_x, e, lde, K, enorm, idx, ws, ws_bytes, 1.0f,
+                       nullptr);
+}
+
+int idf_vq_argmin_x3_ws(void* stream, int64_t P, int32_t D, const float* x, int64_t ld_x,
+                        const uint16_t* ex, int32_t lde, float yscale, int32_t K, const float* enorm,
+                        int32_t* idx, void* ws, int64_t ws_bytes, uint32_t* d_flag) {
+  return vq_argmin_run(true, stream, P, D, x, ld_x, (const float*)ex, lde, K, enorm, idx, ws,
+                       ws_bytes, yscale, d_flag);
 }
 
 int idf_vq_argmin(void* stream, int64_t P, int32_t D, const float* x, int64_t ld_x, const float* e,

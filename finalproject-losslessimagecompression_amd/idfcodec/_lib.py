@@ -157,6 +157,8 @@ SIGNATURES = {
     "idf_vq_norms": (ctypes.c_int, [P, i32, i32, P, i32, P]),
     "idf_vq_argmin": (ctypes.c_int, [P, i64, i32, P, i64, P, i32, i32, P, P]),
     "idf_vq_argmin_ws": (ctypes.c_int, [P, i64, i32, P, i64, P, i32, i32, P, P, P, i64]),
+    "idf_vq_argmin_x3_ws": (ctypes.c_int, [P, i64, i32, P, i64, P, i32, f32, i32, P, P,
+                                           P, i64, P]),
     "idf_vq_argmin_workspace_bytes": (i64, [i64, i32]),
     "idf_vq_gather": (ctypes.c_int, [P, i64, i32, P, P, i32, P, i64]),
     "idf_vq_pointwise": (ctypes.c_int, [P, i64, i32, i32, P, i64, P, i64, P, i64]),

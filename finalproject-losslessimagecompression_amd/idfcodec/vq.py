@@ -235,6 +235,9 @@ class VQEngine:
     """Device VQ-VAE: indices and reconstruction of a batch of images.
 
     conv_mode ("x3t" default, IDF_VQ_CONV overrides; VQ_CONV_MODES): the arithmetic of the convs.
+    argmin_mode ("x3" default, IDF_VQ_ARGMIN overrides; "f32"): the codebook search's x.e products
+    (split-f16 MFMA, fp32-class, or fp32 MFMA).  Encoder-side only -- the decoder reads the
+    indices from the stream -- so it is not recorded.
     encode_pm / decode_pm run it and fall back to "f32" for the whole pass when the split-f16
     range guard trips; last_decode_mode is the mode the last decode_pm ran (what the encoder
     records for its receiver)."""
@@ -247,6 +250,9 @@ class VQEngine:
         if self.conv_mode not in VQ_CONV_MODES:
             raise ValueError(f"IDF_VQ_CONV={self.conv_mode!r}: one of {VQ_CONV_MODES}")
         self.last_decode_mode = self.conv_mode
+        self.argmin_mode = os.environ.get("IDF_VQ_ARGMIN", "x3") if wino else "f32"
+        if self.argmin_mode not in ("x3", "f32"):
+            raise ValueError(f"IDF_VQ_ARGMIN={self.argmin_mode!r}: 'x3' or 'f32'")
         # bench timing (tools/bench_residual.py vq_roofline): when a list, every conv and argmin
         # launch appends (kind, algorithmic FLOPs, event before, event after) on its stream
         self.timer = None
@@ -262,6 +268,11 @@ class VQEngine:
         self.enorm = torch.empty(self.K, dtype=torch.float32, device=device)
         check(lib().idf_vq_norms(_lib.stream_ptr(device), self.K, self.D, ptr(self.embed), self.D,
                                  ptr(self.enorm)), "vq norms")
+        self.embed_x3 = None
+        if self.D % 4 == 0:  # split codebook for idf_vq_argmin_x3_ws
+            ex, self.embed_yscale = taps_weights_x3(_np(model.vq.embed.weight).reshape(
+                self.K, 1, self.D))
+            self.embed_x3 = torch.from_numpy(ex.reshape(-1)).to(device)
 
     def _dev(self, st: Stage):
         return (st, [DevConv(c, self.device, self.wino) for c in st.convs])
@@ -401,12 +412,25 @@ class VQEngine:
         idx = torch.empty(B * h * w, dtype=torch.int32, device=self.device)
         nws = int(lib().idf_vq_argmin_workspace_bytes(B * h * w, self.K))
         ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=self.device)
-        t0, t1 = self._timed("argmin", 2.0 * B * h * w * self.D * self.K)
+        split = self.argmin_mode == "x3" and self.embed_x3 is not None
+        if split:
+            self.flag.zero_()
+        t0, t1 = self._timed("argmin_x3" if split else "argmin", 2.0 * B * h * w * self.D * self.K)
+        def fp32():
+            check(lib().idf_vq_argmin_ws(s, B * h * w, self.D, ptr(z), round_up(self.D, 4),
+                                         ptr(self.embed), self.D, self.K, ptr(self.enorm),
+                                         ptr(idx), ptr(ws), nws), "vq argmin")
         t0()
-        check(lib().idf_vq_argmin_ws(s, B * h * w, self.D, ptr(z), round_up(self.D, 4),
-                                     ptr(self.embed), self.D, self.K, ptr(self.enorm), ptr(idx),
-                                     ptr(ws), nws), "vq argmin")
+        if split:
+            check(lib().idf_vq_argmin_x3_ws(s, B * h * w, self.D, ptr(z), round_up(self.D, 4),
+                                            ptr(self.embed_x3), self.D, self.embed_yscale, self.K,
+                                            ptr(self.enorm), ptr(idx), ptr(ws), nws,
+                                            ptr(self.flag)), "vq argmin x3")
+        else:
+            fp32()
         t1()
+        if split and bool(self.flag.item()):  # the range guard: search again in fp32
+            fp32()
         return idx, (h, w), z
 
     def decode_pm(self, idx, B, h, w, mode=None):

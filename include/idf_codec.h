@@ -555,6 +555,15 @@ int idf_vq_argmin_ws(void *stream, int64_t P, int32_t D, const float *d_x, int64
                      void *d_ws, int64_t ws_bytes);
 int idf_vq_argmin(void *stream, int64_t P, int32_t D, const float *d_x, int64_t ld_x,
                   const float *d_e, int32_t lde, int32_t K, const float *d_enorm, int32_t *d_idx);
+/* idf_vq_argmin_ws with x.e_k on split-f16 products (xh.eh + xl.eh + xh.el on
+ * v_mfma_f32_16x16x16_f16, fp32 accumulation): d_ex is the codebook pre-split as for
+ * idf_conv_taps_x3 ([K][lde/4][8] halves of E * 2^k, yscale = 2^-k); |x|^2 and d_enorm stay
+ * fp32.  A NaN or |x| >= 32768 ORs bit 0 into *d_flag: the caller searches again with
+ * idf_vq_argmin_ws.  (The index is encoder-side only: the decoder reads it from the stream.) */
+int idf_vq_argmin_x3_ws(void *stream, int64_t P, int32_t D, const float *d_x, int64_t ld_x,
+                        const uint16_t *d_ex, int32_t lde, float yscale, int32_t K,
+                        const float *d_enorm, int32_t *d_idx, void *d_ws, int64_t ws_bytes,
+                        uint32_t *d_flag);
 /* nn.Embedding lookup: out[p, c] = e[idx[p], c], c < D. */
 int idf_vq_gather(void *stream, int64_t P, int32_t D, const int32_t *d_idx, const float *d_e,
                   int32_t lde, float *d_out, int64_t ld_out);

@@ -165,6 +165,69 @@ def test_vq_argmin_slices_equal_one_pass(P, K, D):
     assert not (one.cpu() == K // 2).any()  # the duplicate of code K // 3 never wins
 
 
+@pytest.mark.parametrize("P,K,D", [(8192, 16384, 512), (1000, 1100, 64), (77, 300, 20)])
+def test_vq_argmin_x3_vs_fp64(P, K, D):
+    """idf_vq_argmin_x3_ws (split-f16 x.e products): sliced and one-pass searches agree bit for
+    bit, the index equals a float64 search (and the fp32 kernel's) wherever the best two codes
+    differ by > 1e-3, ties go to the lowest index, and an input past the f16 pairs' range sets
+    the flag."""
+    from idfcodec import _lib, vq
+    from idfcodec._lib import check, lib, ptr
+    g = torch.Generator().manual_seed(P + K + 1)
+    x = torch.tanh(torch.randn(P, D, generator=g)).cuda()
+    e = (torch.randn(K, D, generator=g) * 0.5)
+    e[K // 2] = e[K // 3]
+    ex, ys = vq.taps_weights_x3(e.double().numpy().reshape(K, 1, D))
+    ex = torch.from_numpy(ex.reshape(-1)).cuda()
+    e = e.cuda()
+    s = _lib.stream_ptr()
+    en = torch.empty(K, device="cuda")
+    check(lib().idf_vq_norms(s, K, D, ptr(e), D, ptr(en)), "norms")
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    nws = int(lib().idf_vq_argmin_workspace_bytes(P, K))
+    ws = torch.empty(max(nws, 1), dtype=torch.uint8, device="cuda")
+    out = {}
+    for name, (w, nw) in {"one": (None, 0), "sliced": (ws, nws)}.items():
+        out[name] = torch.empty(P, dtype=torch.int32, device="cuda")
+        check(lib().idf_vq_argmin_x3_ws(s, P, D, ptr(x), D, ptr(ex), D, ys, K, ptr(en),
+                                        ptr(out[name]), ptr(w) if w is not None else None, nw,
+                                        ptr(flag)), "argmin x3")
+    assert torch.equal(out["one"], out["sliced"])
+    assert int(flag.item()) == 0
+    f32 = torch.empty(P, dtype=torch.int32, device="cuda")
+    check(lib().idf_vq_argmin_ws(s, P, D, ptr(x), D, ptr(e), D, K, ptr(en), ptr(f32), ptr(ws), nws),
+          "argmin")
+    got = out["one"].cpu().long()
+    xd, ed = x.cpu().double(), e.cpu().double()
+    d = (xd ** 2).sum(1, keepdim=True) + (ed ** 2).sum(1) - 2 * xd @ ed.t()
+    srt, order = torch.sort(d, dim=1, stable=True)
+    ok = (srt[:, 1] - srt[:, 0]) > 1e-3
+    assert ok.float().mean() > 0.3
+    assert torch.equal(got[ok], order[ok, 0])
+    assert torch.equal(got[ok], f32.cpu().long()[ok])
+    assert not (got == K // 2).any()
+    x[P // 2, D // 2] = 40000.0
+    check(lib().idf_vq_argmin_x3_ws(s, P, D, ptr(x), D, ptr(ex), D, ys, K, ptr(en),
+                                    ptr(out["one"]), None, 0, ptr(flag)), "argmin x3")
+    assert int(flag.item()) == 1
+
+
+def test_vq_engine_argmin_modes_agree():
+    """VQEngine's split-f16 codebook search (argmin_mode "x3", the default) and the fp32 one give
+    the same indices on the reference's encoder data wherever its margin exceeds 1e-4."""
+    m, z = model_for("vq_t1_3down")
+    eng = m.engine()
+    data = torch.from_numpy(z["data"]).cuda()
+    got = {}
+    for mode in ("x3", "f32"):
+        eng.argmin_mode = mode
+        got[mode] = m.indices(data).cpu().numpy()
+    eng.argmin_mode = "x3"
+    ok = z["d_margin"].reshape(got["x3"].shape) > 1e-4
+    assert np.array_equal(got["x3"][ok], got["f32"][ok])
+    assert np.array_equal(got["x3"][ok], z["idx"][ok])
+
+
 @pytest.mark.parametrize("kind,ci,co,H,W", [("conv4s2", 3, 128, 64, 64), ("conv4s2", 128, 256, 32, 32),
                                             ("conv3", 40, 24, 9, 7), ("conv1", 384, 512, 8, 8),
                                             ("convT", 384, 256, 8, 8), ("convT", 256, 3, 16, 16)])

@@ -96,12 +96,15 @@ def flow_conv_roofline(codec, fl, img):
 VQ_PEAK = {"conv_taps": ("f32 MFMA", 157.3), "argmin": ("f32 MFMA", 157.3),
            "conv_taps_x3": ("f16 MFMA (split-f16 products)", 2500.0),
            "resblock3x3_x3": ("f16 MFMA (split-f16 products)", 2500.0),
-           "resblock3x3_f32": ("f32 MFMA", 157.3)}
+           "resblock3x3_f32": ("f32 MFMA", 157.3),
+           "argmin_x3": ("f16 MFMA (split-f16 products)", 2500.0)}
 VQ_KERNEL = {"conv_taps": "conv_taps_kernel (strided / transposed VQ-VAE convs as tap GEMMs)",
              "conv_taps_x3": "conv_taps_kernel<..., X3=true> (the tap GEMMs with split-f16 "
                              "products on v_mfma_f32_16x16x16_f16, VQ conv mode x3t)",
              "argmin": "vq_argmin_kernel (+vq_argmin_merge_kernel): fused distance + running "
                        "min over the codebook, 2*D*K FLOP per latent",
+             "argmin_x3": "vq_argmin_kernel<true> (+merge): the codebook search with split-f16 "
+                          "x.e products on v_mfma_f32_16x16x16_f16, 2*D*K FLOP per latent",
              "resblock3x3_x3": "conv3_wino_kernel<..., true, ...> via idf_conv3x3_wx3_res "
                                "(ResBlock 3x3, split-f16 Winograd, residual fused)",
              "resblock3x3_f32": "conv3_wino_kernel via idf_conv3x3_wino_res (exact f32)"}
