@@ -109,7 +109,7 @@ def conv_source_hash() -> str:
 
 def pmc_traffic(kernels, n_last: int, extra: str = "conv3_wino_reduce_kernel"):
     """HBM bytes per launch of the DenseLayer conv from the newest committed PMC passes
-    (profiles/<round>/pmc_bench/{fetch,write}.csv, written by tools/pmc_bench.sh over this
+    (profiles/<round>/pmc_bench/{fetch,write}.csv[.gz], written by tools/pmc_bench.sh over this
     bench), over the same launches as roofline.achieved: the process's last n_last dispatches
     whose name contains one of `kernels` (the sampled encode pass ends the run) plus the `extra`
     dispatches among them (the 8x8 split-K reduce, whose time roofline_pass also counts).
@@ -119,7 +119,7 @@ def pmc_traffic(kernels, n_last: int, extra: str = "conv3_wino_reduce_kernel"):
     conv_source_hash())."""
     import csv
     import glob
-    fetch = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_bench", "fetch.csv")))
+    fetch = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_bench", "fetch.csv*")))
     if not fetch or n_last <= 0:
         return None, None
     d = os.path.dirname(fetch[-1])
@@ -131,10 +131,15 @@ def pmc_traffic(kernels, n_last: int, extra: str = "conv3_wino_reduce_kernel"):
                       f"(hash {have or 'unrecorded'} != built {want[:16]}); not reported")
 
     def total(name):
+        import gzip
         path = os.path.join(d, name)
+        opener = open
+        if os.path.exists(path + ".gz"):
+            path, opener = path + ".gz", gzip.open
         if not os.path.exists(path):
             return None
-        rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Dispatch_Id"]))
+        with opener(path, "rt", newline="") as fh:
+            rows = sorted(csv.DictReader(fh), key=lambda r: int(r["Dispatch_Id"]))
         main = [r for r in rows if any(k in r["Kernel_Name"] for k in kernels)]
         if len(main) < n_last:
             return None
