@@ -1182,18 +1182,73 @@ __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_block_kernel(Dx3Args 
 // ORs bit 0 of flag for a value that is NaN or |x| >= 32768 (the f16 pairs' range).  One
 // thread per (pixel, 4 channels).  Threads [0, nzero) also clear zero[] (the split-K tile
 // counters of the block's dx3 layers, idf_conv3x3_dx3: zero before a block's first layer).
+// With hacc (c0 = 0; the fused head of a block run as per-layer launches) the same launch
+// starts the head's running sums, dx3_head_init_kernel's arithmetic: the thread of a pixel's
+// quad k < 4 forms outputs 4k .. 4k + 3, each bias[o] then c = 0 .. c1 - 1 in order,
+// fmaf(w[o][c], x[c], .) -- the same chain, so the same bits (one thread per pixel and 16
+// outputs in its own range of the launch measured slower: 24.2 vs 20.3 ms over the bench
+// profile, against 14.2 + 9.5 for the two launches, profiles/r06/head_split/).
+// pixel p's running head sums from the block input (dx3_head_init_kernel's per-pixel body)
+__device__ __forceinline__ void dx3_head_init_pixel(int64_t p, int32_t C0, const float* __restrict__ x,
+                                                    int64_t ld_x, const float* __restrict__ w,
+                                                    int32_t ldw, const float* __restrict__ bias,
+                                                    int32_t nh, float* __restrict__ acc) {
+  float h[16];
+#pragma unroll
+  for (int o = 0; o < 16; ++o) h[o] = o < nh ? bias[o] : 0.0f;
+  const float* xr = x + p * ld_x;
+  for (int c = 0; c < C0; c += 4) {
+    const d4 xv = *(const d4*)(xr + c);
+#pragma unroll
+    for (int o = 0; o < 16; ++o) {
+      if (o >= nh) break;
+      const d4 wv = *(const d4*)(w + (int64_t)o * ldw + c);  // uniform: one scalar 16-B load
+#pragma unroll
+      for (int k = 0; k < 4; ++k) h[o] = __builtin_fmaf(wv[k], xv[k], h[o]);
+    }
+  }
+  d4* ap = (d4*)(acc + p * 16);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ap[i] = d4{h[4 * i], h[4 * i + 1], h[4 * i + 2], h[4 * i + 3]};
+}
+
+struct Dx3HeadInit {
+  const float* w;
+  int32_t ldw;
+  const float* bias;
+  int32_t nh;
+  float* acc;  // [P][16]
+};
 __global__ void __launch_bounds__(256) dx3_split_cols_kernel(int64_t P, int32_t c0, int32_t c1,
                                                              const float* __restrict__ x,
                                                              int64_t ld_x, uint16_t* __restrict__ xs,
                                                              uint32_t* __restrict__ flag,
                                                              uint32_t* __restrict__ zero,
-                                                             int32_t nzero) {
+                                                             int32_t nzero, Dx3HeadInit hi) {
   const int nq = ((c1 + 15) / 16 * 16 - c0) / 4;  // channel quads per pixel
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g < nzero) zero[g] = 0u;
   if (g >= P * nq) return;
   const int64_t pix = g / nq;
-  const int c = c0 + 4 * (int)(g - pix * nq);
+  const int kq = (int)(g - pix * nq);
+  const int c = c0 + 4 * kq;
+  if (hi.acc && kq < 4) {
+    d4 h;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h[i] = 4 * kq + i < hi.nh ? hi.bias[4 * kq + i] : 0.0f;
+    const float* xr = x + pix * ld_x;
+    for (int cc = 0; cc < c1; cc += 4) {
+      const d4 xv = *(const d4*)(xr + cc);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (4 * kq + i >= hi.nh) break;
+        const d4 wv = *(const d4*)(hi.w + (int64_t)(4 * kq + i) * hi.ldw + cc);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) h[i] = __builtin_fmaf(wv[k], xv[k], h[i]);
+      }
+    }
+    *(d4*)(hi.acc + pix * 16 + 4 * kq) = h;
+  }
   d4 v = d4{0.f, 0.f, 0.f, 0.f};
   if (c < c1) v = *(const d4*)(x + pix * ld_x + c);  // c1 % 4 == 0: a quad is all in or all out
   const e4 h = __builtin_convertvector(v, e4);
@@ -1375,10 +1430,17 @@ extern "C" int64_t idf_conv3x3_dx3_workspace(int32_t B, int32_t H, int32_t W, in
   return idf_conv3x3_dx3_counter_bytes(B, H, W, N) + s.part_bytes;
 }
 
-extern "C" int idf_dx3_split_cols(void* stream, int64_t P, int32_t c0, int32_t c1, const float* x,
-                                  int64_t ld_x, uint16_t* xs, int32_t nslab_xs, uint32_t* d_flag,
-                                  uint32_t* d_zero, int32_t nzero) {
+// the split (and, with head, the head init fused into the same launch)
+static int dx3_split_cols_run(void* stream, int64_t P, int32_t c0, int32_t c1, const float* x,
+                              int64_t ld_x, uint16_t* xs, int32_t nslab_xs, uint32_t* d_flag,
+                              uint32_t* d_zero, int32_t nzero, const Dx3HeadInit& head) {
   if (P < 0 || c1 < c0 || nzero < 0 || (nzero && !d_zero)) return IDF_ERR_ARG;
+  if (head.acc) {  // idf_dx3_head_init's contract, over the block input c0 = 0 .. c1
+    if (P == 0) return IDF_OK;
+    if (c0 != 0 || c1 <= 0 || !head.w || !head.bias || head.nh < 1 || head.nh > 16 || c1 > 64 ||
+        head.ldw < c1 || (head.ldw & 3) || (uintptr_t)head.w % 16 || (uintptr_t)head.acc % 16)
+      return IDF_ERR_ARG;
+  }
   if (P == 0 || c1 == c0) {
     if (nzero) return hipMemsetAsync(d_zero, 0, 4 * (size_t)nzero, (hipStream_t)stream) == hipSuccess
                           ? IDF_OK : IDF_ERR_HIP;
@@ -1389,8 +1451,26 @@ extern "C" int idf_dx3_split_cols(void* stream, int64_t P, int32_t c0, int32_t c
   int64_t n = P * (((c1 + 15) / 16 * 16 - c0) / 4);
   if (n < nzero) n = nzero;
   hipLaunchKernelGGL(dx3_split_cols_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, P, c0, c1, x, ld_x, xs, d_flag, d_zero, nzero);
+                     (hipStream_t)stream, P, c0, c1, x, ld_x, xs, d_flag, d_zero, nzero, head);
   return idf_last_error();
+}
+
+extern "C" int idf_dx3_split_cols(void* stream, int64_t P, int32_t c0, int32_t c1, const float* x,
+                                  int64_t ld_x, uint16_t* xs, int32_t nslab_xs, uint32_t* d_flag,
+                                  uint32_t* d_zero, int32_t nzero) {
+  return dx3_split_cols_run(stream, P, c0, c1, x, ld_x, xs, nslab_xs, d_flag, d_zero, nzero,
+                            Dx3HeadInit{});
+}
+
+// the block input's split copy and the fused head's running sums in one launch (flow_kernels
+// dense_block_run; the same bits as idf_dx3_split_cols + idf_dx3_head_init)
+int idf_dx3_split_cols_head(void* stream, int64_t P, int32_t c1, const float* x, int64_t ld_x,
+                            uint16_t* xs, int32_t nslab_xs, uint32_t* d_flag, uint32_t* d_zero,
+                            int32_t nzero, const float* w, int32_t ldw, const float* bias,
+                            int32_t n_head, float* acc) {
+  if (!acc) return IDF_ERR_ARG;
+  return dx3_split_cols_run(stream, P, 0, c1, x, ld_x, xs, nslab_xs, d_flag, d_zero, nzero,
+                            Dx3HeadInit{w, ldw, bias, n_head, acc});
 }
 
 #ifndef IDF_HEAD_INIT_EXTERNAL  // tools/repro_lds builds link a variant head init instead
@@ -1408,23 +1488,7 @@ __global__ void __launch_bounds__(256) dx3_head_init_kernel(int64_t P, int32_t C
                                                             int32_t nh, float* __restrict__ acc) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
-  float h[16];
-#pragma unroll
-  for (int o = 0; o < 16; ++o) h[o] = o < nh ? bias[o] : 0.0f;
-  const float* xr = x + p * ld_x;
-  for (int c = 0; c < C0; c += 4) {
-    const d4 xv = *(const d4*)(xr + c);
-#pragma unroll
-    for (int o = 0; o < 16; ++o) {
-      if (o >= nh) break;
-      const d4 wv = *(const d4*)(w + (int64_t)o * ldw + c);  // uniform: one scalar 16-B load
-#pragma unroll
-      for (int k = 0; k < 4; ++k) h[o] = __builtin_fmaf(wv[k], xv[k], h[o]);
-    }
-  }
-  d4* ap = (d4*)(acc + p * 16);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) ap[i] = d4{h[4 * i], h[4 * i + 1], h[4 * i + 2], h[4 * i + 3]};
+  dx3_head_init_pixel(p, C0, x, ld_x, w, ldw, bias, nh, acc);
 }
 
 extern "C" int idf_dx3_head_init(void* stream, int64_t P, int32_t C0, const float* x, int64_t ld_x,

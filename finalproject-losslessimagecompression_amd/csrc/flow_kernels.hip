@@ -721,14 +721,21 @@ static int dense_block_run(void* stream, const IdfDenseBlock* blk, int32_t B, in
     dws_bytes = need;
     if (pl.fuse) hacc = (float*)((char*)tmp + pl.hoff);
     const int64_t ctr = idf_conv3x3_dx3_counter_bytes(B, H, W, blk->g_pad);
+    // the head init rides in the split's launch where it can (same bits, one launch fewer)
+    const bool head_in_split = !dxb && hacc && !fused && blk->k_in[0] > 0 && blk->k_in[0] <= 64;
     int rc = dxb ? idf_dxb_cols(stream, P, 0, blk->k_in[0], feat, ld_feat, xs, nslab_xs,
                                 need > 0 ? (uint32_t*)dws : nullptr,
                                 need > 0 ? (int32_t)(ctr / 4) : 0)
-                 : idf_dx3_split_cols(stream, P, 0, blk->k_in[0], feat, ld_feat, xs, nslab_xs,
-                                      blk->range_flag, need > 0 ? (uint32_t*)dws : nullptr,
-                                      need > 0 ? (int32_t)(ctr / 4) : 0);
+           : head_in_split
+               ? idf_dx3_split_cols_head(stream, P, blk->k_in[0], feat, ld_feat, xs, nslab_xs,
+                                         blk->range_flag, need > 0 ? (uint32_t*)dws : nullptr,
+                                         need > 0 ? (int32_t)(ctr / 4) : 0, blk->wh, blk->ldwh,
+                                         blk->bh, blk->n_head, hacc)
+               : idf_dx3_split_cols(stream, P, 0, blk->k_in[0], feat, ld_feat, xs, nslab_xs,
+                                    blk->range_flag, need > 0 ? (uint32_t*)dws : nullptr,
+                                    need > 0 ? (int32_t)(ctr / 4) : 0);
     if (rc) return rc;
-    if (hacc && !fused) {
+    if (hacc && !fused && !head_in_split) {
       rc = idf_dx3_head_init(stream, P, blk->k_in[0], feat, ld_feat, blk->wh, blk->ldwh, blk->bh,
                              blk->n_head, hacc);
       if (rc) return rc;
