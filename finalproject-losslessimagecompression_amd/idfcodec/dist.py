@@ -430,7 +430,10 @@ def agree_shards(bs, group=None, vq_conv=None):
     from .codec import CONV_CODES
     code = CONV_CODES.get(bs.meta.get("conv", "f32"), -1)
     scratch = int("scratch_offsets" in bs.meta)
-    vq = {None: 0, "f32": 1, "x3": 2}[vq_conv]
+    vq_modes = (None, "f32", "x3", "x3t")  # idfcodec.vq.VQ_CONV_MODES, and "no VQ"
+    if vq_conv not in vq_modes:
+        raise ValueError(f"unknown VQ conv mode {vq_conv!r}")
+    vq = vq_modes.index(vq_conv)
     v = torch.tensor([code, -code, bs.n_images, -bs.n_images, scratch, vq, -vq],
                      dtype=torch.int64)
     dist.all_reduce(v, op=dist.ReduceOp.MAX, group=host_group(group))

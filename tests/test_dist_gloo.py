@@ -84,7 +84,7 @@ def test_shard_range_covers():
             assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
 
 
-def _res_worker(rank, world, port, out):
+def _res_worker(rank, world, port, out, vq_conv="f32"):
     import sys
     sys.path.insert(0, PKG)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -95,9 +95,10 @@ def _res_worker(rank, world, port, out):
     st, nw, w = _fake_shard(rank, 2, 3)
     flow = Bitstream(3, [(6, 4, 4), (12, 2, 2)], st, nw, w, meta={"n_subpixels": 3 * 192})
     idx = torch.arange(5, dtype=torch.int32) + 100 * rank  # 5 words: 3 images x 1..2 words
-    rbs = ResidualBitstream(flow, idx, 3, (3, 8, 8), (2, 2), 8192)
+    rbs = ResidualBitstream(flow, idx, 3, (3, 8, 8), (2, 2), 8192, vq_conv=vq_conv)
     res = gather_residual(rbs)
     if rank == 0:
+        assert res.vq_conv == vq_conv
         torch.save({"st": res.flow.states, "idx": res.idx_words, "n": res.n_images,
                     "ns": res.flow.meta["n_subpixels"]}, out)
     else:
@@ -106,11 +107,14 @@ def _res_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_gather_residual_two_ranks(tmp_path):
+@pytest.mark.parametrize("vq_conv", ["f32", "x3", "x3t"])
+def test_gather_residual_two_ranks(tmp_path, vq_conv):
     """configs 4/5 (8 x MI355X, batch-sharded): the residual bitstreams of two ranks merge on
-    rank 0 -- flow streams in single-batch order, index code runs in rank order."""
+    rank 0 -- flow streams in single-batch order, index code runs in rank order -- for every
+    VQ conv mode (round 6's default "x3t" included: the one-GPU N=2 rehearsal found it
+    missing from agree_shards)."""
     out = str(tmp_path / "r.pt")
-    mp.spawn(_res_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    mp.spawn(_res_worker, args=(2, _free_port(), out, vq_conv), nprocs=2, join=True)
     r = torch.load(out, weights_only=True)
     assert r["n"] == 6 and r["ns"] == 6 * 192
     assert torch.equal(r["idx"], torch.cat([torch.arange(5) + 100 * k for k in range(2)]).int())
