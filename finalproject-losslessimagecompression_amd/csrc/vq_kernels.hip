@@ -19,6 +19,8 @@
 // ties go to the lowest index (torch.argmin).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <utility>
+#include <type_traits>
 
 #include "idf_codec_internal.h"
 
@@ -59,6 +61,16 @@ struct ConvTapsArgs {
   uint32_t* flag;
 };
 
+// f(integral_constant<int, T>) for T = 0 .. N - 1 in order
+template <int N, typename F, int... T>
+__device__ __forceinline__ void dx_taps_unroll_impl(F&& f, std::integer_sequence<int, T...>) {
+  (f(std::integral_constant<int, T>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void dx_taps_unroll(F&& f) {
+  dx_taps_unroll_impl<N>(f, std::make_integer_sequence<int, N>{});
+}
+
 __device__ __forceinline__ float vq_act(float v, int act, float slope) {
   if (act == IDF_ACT_RELU) return v > 0.0f ? v : 0.0f;
   if (act == IDF_ACT_LEAKY) return v > 0.0f ? v : v * slope;
@@ -70,7 +82,13 @@ __device__ __forceinline__ float vq_act(float v, int act, float slope) {
 // v_mfma_f32_16x16x16_f16 (x = xh + xl split when the tile is staged, the weights pre-split on
 // the host): xh.wh + xl.wh + xh.wl per k-step, fp32 accumulation -- the split-f16 arithmetic of
 // the flow's dx3 / wx3 convs, 1/16 of the MFMA cycles of the fp32 16x16x4 steps it replaces.
-template <int BM, int BN, int WAVES_M, int WAVES_N, bool X3>
+// R: k-chunks whose global loads are in flight in registers (R - 1 ahead of the chunk being
+// multiplied; two LDS stages either way).  Which chunk meets which accumulator in which order
+// does not depend on R: the outputs are bit-identical for every R.
+#ifndef IDF_TAPS_PREFETCH
+#define IDF_TAPS_PREFETCH 3
+#endif
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool X3, int R>
 __global__ void __launch_bounds__(256) conv_taps_kernel(ConvTapsArgs g) {
   constexpr int BK = 16;
   constexpr int LDS_LD = BK + 8;  // conflict-free b128 fragment reads
@@ -109,9 +127,9 @@ __global__ void __launch_bounds__(256) conv_taps_kernel(ConvTapsArgs g) {
   }
   const int nslab = (g.C + BK - 1) / BK;
   const int nk = nslab * g.ntaps;
-  f4 ra[A_PER_T], rb[B_PER_T];
+  f4 ra_s[R][A_PER_T], rb_s[R][B_PER_T];
 
-  auto load_chunk = [&](int kc) {
+  auto load_chunk = [&](int kc, f4 (&ra)[A_PER_T], f4 (&rb)[B_PER_T]) {
     const int slab = kc / g.ntaps, tap = kc - slab * g.ntaps, c0 = slab * BK;
     const int dy = g.dy[tap], dx = g.dx[tap];
 #pragma unroll
@@ -132,7 +150,7 @@ __global__ void __launch_bounds__(256) conv_taps_kernel(ConvTapsArgs g) {
     }
   };
   bool in_ok = true;
-  auto store_chunk = [&](int buf) {
+  auto store_chunk = [&](int buf, const f4 (&ra)[A_PER_T], const f4 (&rb)[B_PER_T]) {
 #pragma unroll
     for (int j = 0; j < A_PER_T; ++j) {
       if constexpr (X3) {  // (xh[4], xl[4]) in the 16 bytes of the 4 fp32 values
@@ -161,13 +179,16 @@ __global__ void __launch_bounds__(256) conv_taps_kernel(ConvTapsArgs g) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
-  load_chunk(0);
-  store_chunk(0);
+#pragma unroll
+  for (int j = 0; j < R - 1; ++j)
+    if (j < nk) load_chunk(j, ra_s[j], rb_s[j]);
+  store_chunk(0, ra_s[0], rb_s[0]);
   __syncthreads();
   const int lr = lane & 15, lk = 4 * (lane >> 4);
-  for (int kc = 0; kc < nk; ++kc) {
+  auto step = [&](int kc, f4 (&ra_next)[A_PER_T], f4 (&rb_next)[B_PER_T],
+                  const f4 (&ra_st)[A_PER_T], const f4 (&rb_st)[B_PER_T]) {
     const int buf = kc & 1;
-    if (kc + 1 < nk) load_chunk(kc + 1);
+    if (kc + R - 1 < nk) load_chunk(kc + R - 1, ra_next, rb_next);
     f4 fa[FM], fb[FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i) fa[i] = *(const f4*)&As[buf][wm * WTM + i * 16 + lr][lk];
@@ -198,8 +219,18 @@ __global__ void __launch_bounds__(256) conv_taps_kernel(ConvTapsArgs g) {
           for (int j = 0; j < FN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][t], fb[j][t], acc[i][j], 0, 0, 0);
     }
-    if (kc + 1 < nk) store_chunk(buf ^ 1);
+    if (kc + 1 < nk) store_chunk(buf ^ 1, ra_st, rb_st);
     __syncthreads();
+  };
+  for (int kc0 = 0; kc0 < nk; kc0 += R) {
+    // chunk kc0 + t: loads chunk kc0 + t + R - 1 into set (t + R - 1) % R, stages chunk
+    // kc0 + t + 1 from set (t + 1) % R (kc0 is a multiple of R)
+    dx_taps_unroll<R>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      if (kc0 + t < nk)
+        step(kc0 + t, ra_s[(t + R - 1) % R], rb_s[(t + R - 1) % R], ra_s[(t + 1) % R],
+             rb_s[(t + 1) % R]);
+    });
   }
 
   // bias loads first (a load after a store to a possibly aliasing pointer would wait for it),
@@ -241,7 +272,8 @@ static int launch_taps(ConvTapsArgs a, hipStream_t s) {
   constexpr int BM = 64;
   a.m_tiles = (int)((a.P + BM - 1) / BM);
   a.n_tiles = (a.N + BN - 1) / BN;
-  hipLaunchKernelGGL((conv_taps_kernel<BM, BN, WM, WN, X3>), dim3((unsigned)(a.m_tiles * a.n_tiles)),
+  hipLaunchKernelGGL((conv_taps_kernel<BM, BN, WM, WN, X3, IDF_TAPS_PREFETCH>),
+                     dim3((unsigned)(a.m_tiles * a.n_tiles)),
                      dim3(256), 0, s, a);
   return idf_last_error();
 }
