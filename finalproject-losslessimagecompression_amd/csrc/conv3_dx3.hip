@@ -1464,7 +1464,7 @@ extern "C" int idf_dx3_split_cols(void* stream, int64_t P, int32_t c0, int32_t c
 
 // the block input's split copy and the fused head's running sums in one launch (flow_kernels
 // dense_block_run; the same bits as idf_dx3_split_cols + idf_dx3_head_init)
-int idf_dx3_split_cols_head(void* stream, int64_t P, int32_t c1, const float* x, int64_t ld_x,
+extern "C" int idf_dx3_split_cols_head(void* stream, int64_t P, int32_t c1, const float* x, int64_t ld_x,
                             uint16_t* xs, int32_t nslab_xs, uint32_t* d_flag, uint32_t* d_zero,
                             int32_t nzero, const float* w, int32_t ldw, const float* bias,
                             int32_t n_head, float* acc) {

@@ -31,12 +31,6 @@ struct IdfDx3BlockDesc {
   const float* hb;               // the head bias
 };
 int idf_dx3_block_launch(void* stream, const IdfDx3BlockDesc* d);
-// idf_dx3_split_cols (c0 = 0) and idf_dx3_head_init over the same block input in one launch
-// (conv3_dx3.hip; the same bits as the two calls)
-int idf_dx3_split_cols_head(void* stream, int64_t P, int32_t c1, const float* x, int64_t ld_x,
-                            uint16_t* xs, int32_t nslab_xs, uint32_t* d_flag, uint32_t* d_zero,
-                            int32_t nzero, const float* w, int32_t ldw, const float* bias,
-                            int32_t n_head, float* acc);
 
 // marker written by rans_cdf_freq for scale == 0 (freq can never be INT32_MIN)
 #define IDF_FREQ_SCALE_ZERO ((int32_t)0x80000000)

@@ -130,6 +130,8 @@ SIGNATURES = {
     "idf_conv3x3_dx3_workspace": (i64, [i32, i32, i32, i32, i32]),
     "idf_dx3_split_bytes": (i64, [i64, i32]),
     "idf_dx3_split_cols": (ctypes.c_int, [P, i64, i32, i32, P, i64, P, i32, P, P, i32]),
+    "idf_dx3_split_cols_head": (ctypes.c_int, [P, i64, i32, P, i64, P, i32, P, P, i32, P, i32, P,
+                                               i32, P]),
     "idf_conv3x3_dxb_supported": (ctypes.c_int, [i32, i32, i32]),
     "idf_conv3x3_dxb": (ctypes.c_int, [P, i32, i32, i32, i32, P, i32, P, i32, P, P, i32, P, i32,
                                        P, i64, i32, f32, P, i64, P]),

@@ -420,6 +420,13 @@ typedef struct IdfDx3Head {
 int idf_dx3_head_init(void *stream, int64_t P, int32_t C0, const float *d_x, int64_t ld_x,
                       const float *d_w, int32_t ldw, const float *d_bias, int32_t n_head,
                       float *d_acc);
+/* idf_dx3_split_cols (c0 = 0, 0 < c1 <= 64) and idf_dx3_head_init (C0 = c1) over the same block
+ * input in ONE launch, bit for bit the two calls' results (each head output's FMA chain is the
+ * same); what idf_dense_block_f32 runs before a per-layer DenseBlock with a fused head. */
+int idf_dx3_split_cols_head(void *stream, int64_t P, int32_t c1, const float *d_x, int64_t ld_x,
+                            uint16_t *d_xs, int32_t nslab_xs, uint32_t *d_flag, uint32_t *d_zero,
+                            int32_t nzero, const float *d_w, int32_t ldw, const float *d_bias,
+                            int32_t n_head, float *d_acc);
 int idf_conv3x3_dx3(void *stream, int32_t B, int32_t H, int32_t W, int32_t C, uint16_t *d_xs,
                     int32_t nslab_xs, const uint16_t *d_w, int32_t nft, float yscale,
                     const float *d_b3, const float *d_vtap, int32_t ldv, const float *d_bfull,

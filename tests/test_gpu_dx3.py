@@ -540,3 +540,47 @@ def test_fused_block_kernel_bit_identical(name, lvl, which):
     assert torch.isfinite(o0).all() and o0.abs().sum() > 0
     assert torch.equal(o0, o1), int((o0 != o1).any(1).sum())
     assert torch.equal(f0, f1), int((f0 != f1).any(1).sum())
+
+
+@pytest.mark.parametrize("P,C0,nh,ld,nslab", [(262144, 8, 12, 544, 2), (16384, 28, 16, 96, 3),
+                                               (1000, 64, 5, 64, 4), (77, 4, 1, 8, 1)])
+def test_split_cols_head_one_launch_bit_identical(P, C0, nh, ld, nslab):
+    """idf_dx3_split_cols_head (what a per-layer DenseBlock with a fused head runs before its
+    first layer) writes the same split copy, range flag, cleared counters and head sums, bit for
+    bit, as idf_dx3_split_cols + idf_dx3_head_init; a NaN input still sets the flag."""
+    from idfcodec import _lib
+    from idfcodec._lib import check, lib, ptr
+    g = torch.Generator().manual_seed(P + C0)
+    x = (torch.randn(P, ld, generator=g) * 3).cuda()
+    w = torch.randn(nh, 68, generator=g).cuda()
+    b = torch.randn(nh, generator=g).cuda()
+    s = _lib.stream_ptr()
+    res = []
+    for one in (False, True):
+        xs = torch.full((nslab * 2 * P * 16,), 0x7E00, dtype=torch.int16, device="cuda")
+        acc = torch.full((P, 16), float("nan"), device="cuda")
+        flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+        zero = torch.full((37,), 7, dtype=torch.int32, device="cuda")
+        if one:
+            check(lib().idf_dx3_split_cols_head(s, P, C0, ptr(x), ld, ptr(xs), nslab, ptr(flag),
+                                                ptr(zero), 37, ptr(w), 68, ptr(b), nh, ptr(acc)),
+                  "split+head")
+        else:
+            check(lib().idf_dx3_split_cols(s, P, 0, C0, ptr(x), ld, ptr(xs), nslab, ptr(flag),
+                                           ptr(zero), 37), "split")
+            check(lib().idf_dx3_head_init(s, P, C0, ptr(x), ld, ptr(w), 68, ptr(b), nh, ptr(acc)),
+                  "head init")
+        torch.cuda.synchronize()
+        res.append((xs.cpu(), acc.cpu(), int(flag.item()), zero.cpu()))
+    (xa, aa, fa, za), (xb, ab, fb, zb) = res
+    assert torch.equal(xa, xb)
+    assert torch.equal(aa.view(torch.int32), ab.view(torch.int32))
+    assert fa == fb == 0 and int(za.abs().sum()) == 0 and int(zb.abs().sum()) == 0
+    ref = b.cpu().double() + x.cpu().double()[:, :C0] @ w.cpu().double()[:, :C0].t()
+    assert (ab[:, :nh].double() - ref).abs().max() < 1e-4 * (1 + ref.abs().max())
+    assert torch.all(ab[:, nh:] == 0)
+    x[P // 2, C0 - 1] = float("nan")
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    check(lib().idf_dx3_split_cols_head(s, P, C0, ptr(x), ld, ptr(xs), nslab, ptr(flag), None, 0,
+                                        ptr(w), 68, ptr(b), nh, ptr(acc)), "split+head")
+    assert int(flag.item()) == 1
