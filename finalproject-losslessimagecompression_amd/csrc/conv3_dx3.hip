@@ -206,6 +206,11 @@ __device__ unsigned long long g_dx3_tl[4096][8];
 #ifndef IDF_DX3_PRIO_K
 #define IDF_DX3_PRIO_K 4
 #endif
+// mixed rows per wave in the two-tile split-f16 blocks (timing A/B builds only; dx3_block): 1 the
+// older wave of a SIMD takes WR + 1 rows of its half tile, 2 WR - 1
+#ifndef IDF_DX3_MIX
+#define IDF_DX3_MIX 0
+#endif
 // waves per block (timing A/B: 16 = four per SIMD at 2 rows per wave)
 #ifndef IDF_DX3_WAVES
 #define IDF_DX3_WAVES 8
@@ -379,16 +384,24 @@ struct Dx3Tables {
 // One launch's work: ML = false, one layer (conv3_dx3_kernel: a block = a chunk of the slabs of
 // one output group of T tiles); ML = true, every layer of a DenseBlock for one tile
 // (conv3_dx3_block_kernel, T = 1, one output group, no split K).
-template <int NF, int WR, int PITCH, int PLANE_KIB, bool BF, bool ML>
-__device__ __forceinline__ void dx3_block(const Dx3Args& g, const Dx3MLArgs* ml) {
+// WRW: the output rows of this wave (WR: of the block layout's waves).  WRW != WR ("mixed
+// rows", IDF_DX3_MIX): the two waves of a SIMD share the 8 rows of one half tile unequally, the
+// older (waves 0-3) WR + 1 rows, the younger WR - 1 -- the older wave runs ahead at the MFMA
+// pipe (the hardware favours it) and waits at the slab barrier for the younger otherwise
+// (profiles/r05/dma_issue/stamps.log).  Rows per wave change no output's summation order.
+template <int NF, int WR, int PITCH, int PLANE_KIB, bool BF, bool ML, int WRW = WR>
+__device__ __forceinline__ void dx3_block(const Dx3Args& g, const Dx3MLArgs* ml, char* lds) {
   using L = Dx3Lds<NF, WR, PITCH, PLANE_KIB, BF>;
-  constexpr int T = L::T, HR = L::HR, NS = L::NS;
+  constexpr bool MIX = WRW != WR;
+  constexpr int T = L::T, HR = WRW + 2;
+  constexpr int NS = BF ? 2 * HR - 1 : IDF_DX3_PAIRS ? 3 * HR - 1 + 2 * WRW : 5 * HR - 1;
+  static_assert(!MIX || (T == 2 && kDxWaves == 8 && !ML && (WRW == WR + 1 || WRW == WR - 1)),
+                "mixed rows: two tiles of two SIMD pairs, per-layer launches");
   static_assert(L::WST % 1024 == 0, "weight stage must be whole 1-KiB DMA pieces");
   static_assert(L::BYTES <= 160 * 1024, "LDS");
   static_assert(HR >= 3, "the A-fragment reads of a phase take its last three steps");
   static_assert(IDF_DX3_DMAS == 0 || IDF_DX3_DMA0 + IDF_DX3_STAG + (L::PPW - 1) * IDF_DX3_DMAS < NS,
                 "every DMA piece of a slab is issued within the slab's steps");
-  __shared__ __attribute__((aligned(16))) char lds[L::BYTES];
   int* last_flag = (int*)(lds + L::FOFF);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -401,9 +414,12 @@ __device__ __forceinline__ void dx3_block(const Dx3Args& g, const Dx3MLArgs* ml)
   const int grp = udiv_s(rem, g.nblk_tiles);
   const int tb = rem - grp * g.nblk_tiles;
   // the wave's tile and first output row
-  const int tw = wave / (kDxWaves / T);
-  const int r0 = WR * (wave % (kDxWaves / T));
-  d4 hreg[WR];  // ML: the fused head's running sums, registers across the layers
+  // (mixed rows: SIMD s = wave & 3 holds half tile s & 1 of tile s >> 1, its older wave the
+  // first WR + 1 rows)
+  const int tw = MIX ? (wave & 3) >> 1 : wave / (kDxWaves / T);
+  constexpr int WR_OLD = IDF_DX3_MIX == 2 ? WR - 1 : WR + 1;  // the older wave's rows (MIX)
+  const int r0 = MIX ? 2 * WR * (wave & 1) + ((wave & 4) ? WR_OLD : 0) : WR * (wave % (kDxWaves / T));
+  d4 hreg[WRW];  // ML: the fused head's running sums, registers across the layers
   const int nlayers = ML ? ml->nlayers : 1;
   for (int li = 0; li < nlayers; ++li) {
   // (ML) the block's indices passed through an opaque asm: everything derived from them below
@@ -547,11 +563,11 @@ __device__ __forceinline__ void dx3_block(const Dx3Args& g, const Dx3MLArgs* ml)
   // chain, so the sums carry the same bits as the split launches' HBM copy
   if constexpr (ML) if (li == 0) {
 #pragma unroll
-    for (int m = 0; m < WR; ++m) hreg[m] = d4{0.f, 0.f, 0.f, 0.f};
+    for (int m = 0; m < WRW; ++m) hreg[m] = d4{0.f, 0.f, 0.f, 0.f};
     if (g.nh > 0) {
       const bool lane_ok0 = xj < g.Wd && ixj < g.nbx;
 #pragma unroll
-      for (int m = 0; m < WR; ++m) {
+      for (int m = 0; m < WRW; ++m) {
         int iy = iyw, y = uyw + m - iyw * g.H;
         if (g.gut) {
           iy = udiv_s(uyw + m, g.hp);
@@ -615,9 +631,9 @@ __device__ __forceinline__ void dx3_block(const Dx3Args& g, const Dx3MLArgs* ml)
   DX3_TL(1);
 
 
-  d4 acc[WR][NF];
+  d4 acc[WRW][NF];
 #pragma unroll
-  for (int m = 0; m < WR; ++m)
+  for (int m = 0; m < WRW; ++m)
 #pragma unroll
     for (int n = 0; n < NF; ++n) acc[m][n] = d4{0.f, 0.f, 0.f, 0.f};
 
@@ -667,7 +683,7 @@ __device__ __forceinline__ void dx3_block(const Dx3Args& g, const Dx3MLArgs* ml)
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy) {
       const int m = h - dy;
-      if (m < 0 || m >= WR) continue;
+      if (m < 0 || m >= WRW) continue;
 #pragma unroll
       for (int n = 0; n < NF; ++n) mma(A[dy][n], Bv, acc[m][n]);
     }
@@ -742,7 +758,7 @@ __device__ __forceinline__ void dx3_block(const Dx3Args& g, const Dx3MLArgs* ml)
           mma_rows(AS[1], Bv, t);
         } else {
           constexpr int h = t - HR;
-          if constexpr (h < WR) {
+          if constexpr (h < WRW) {
 #pragma unroll
             for (int n = 0; n < NF; ++n) mma(AZ[0][n], Bv, acc[h][n]);
           }
@@ -765,10 +781,10 @@ __device__ __forceinline__ void dx3_block(const Dx3Args& g, const Dx3MLArgs* ml)
       //   F_l [HR, 2HR)        h = t - HR:       [wh(dy,0) ; wh(dy,1)] . [xl(h,0) | xl(h,1)]
       //   G_h [2HR, 3HR-1)     h = t - 2HR:      [wh(0,2) ; wh(1,2)], [wl(0,2) ; wl(1,2)] (row h),
       //                                          [0 ; wl(2,2)] (row h - 1) . [xh(h,2) | xh(h+1,2)]
-      //   G_l [3HR-1, +WR)     h = t - 3HR + 1:  [wh(0,2) ; wh(1,2)] . [xl(h,2) | xl(h+1,2)]
+      //   G_l [3HR-1, +WRW)     h = t - 3HR + 1:  [wh(0,2) ; wh(1,2)] . [xl(h,2) | xl(h+1,2)]
       //   P   [TP, NS)         m = t - TP:       [wh(2,2) ; wh(2,2)] . [xh | xl](m + 2, 2)
-      constexpr int TL = HR, TG = 2 * HR, TGL = 3 * HR - 1, TP = TGL + WR;
-      static_assert(BF || TP + WR == NS, "the paired schedule's steps");
+      constexpr int TL = HR, TG = 2 * HR, TGL = 3 * HR - 1, TP = TGL + WRW;
+      static_assert(BF || TP + WRW == NS, "the paired schedule's steps");
       e8 AH[3][NF], AL[3][NF], GH[NF], GL[NF], GZ[NF], PW[NF];
       auto read_Bp = [&](const char* st, int t) -> e8 {
         if (t < TL) return rdB(st + oF + t * PITCH * 32);
@@ -817,7 +833,7 @@ __device__ __forceinline__ void dx3_block(const Dx3Args& g, const Dx3MLArgs* ml)
           mma_rows(AH, Bv, t - TL);
         } else if constexpr (t < TGL) {
           constexpr int h = t - TG;
-          if constexpr (h < WR) {
+          if constexpr (h < WRW) {
 #pragma unroll
             for (int n = 0; n < NF; ++n) mma(GH[n], Bv, acc[h][n]);
           }
@@ -825,7 +841,7 @@ __device__ __forceinline__ void dx3_block(const Dx3Args& g, const Dx3MLArgs* ml)
 #pragma unroll
             for (int n = 0; n < NF; ++n) mma(GZ[n], Bv, acc[h - 1][n]);
           }
-          if constexpr (h < WR) {
+          if constexpr (h < WRW) {
 #pragma unroll
             for (int n = 0; n < NF; ++n) mma(GL[n], Bv, acc[h][n]);
           }
@@ -888,7 +904,7 @@ __device__ __forceinline__ void dx3_block(const Dx3Args& g, const Dx3MLArgs* ml)
         mma_rows(AS[1], Bv, t - 3 * HR);
       } else {
         constexpr int h = t - 4 * HR;
-        if constexpr (h < WR) {
+        if constexpr (h < WRW) {
 #pragma unroll
           for (int n = 0; n < NF; ++n) mma(AZ[0][n], Bv, acc[h][n]);
         }
@@ -927,10 +943,10 @@ __device__ __forceinline__ void dx3_block(const Dx3Args& g, const Dx3MLArgs* ml)
     const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(
         (void*)g.part, 0, (int)(pbytes < (int64_t)kDxInvalid ? pbytes : (int64_t)kDxInvalid), 0x00020000);
     auto poff = [&](int c, int m, int n) -> uint32_t {
-      return pb + (uint32_t)((c * FR + (wave * WR + m) * NF + n) * 1024 + lane * 16);
+      return pb + (uint32_t)((c * FR + (tw * 16 + r0 + m) * NF + n) * 1024 + lane * 16);
     };
 #pragma unroll
-    for (int m = 0; m < WR; ++m)
+    for (int m = 0; m < WRW; ++m)
 #pragma unroll
       for (int n = 0; n < NF; ++n)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[m][n]), pr, poff(chunk, m, n),
@@ -952,18 +968,18 @@ __device__ __forceinline__ void dx3_block(const Dx3Args& g, const Dx3MLArgs* ml)
     // every other chunk's fragments in flight at once (one memory round trip, not nchunk), then
     // the sums in chunk order; chunk slots past nchunk and the block's own read nothing
     static_assert(IDF_DX3_KSPLIT <= 4, "the reduction holds up to 4 chunks");
-    d4 pv[4][WR][NF];
+    d4 pv[4][WRW][NF];
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
-      for (int m = 0; m < WR; ++m)
+      for (int m = 0; m < WRW; ++m)
 #pragma unroll
         for (int n = 0; n < NF; ++n)
           pv[c][m][n] = (c < Ly.nchunk && c != chunk)
                             ? __builtin_bit_cast(d4, __builtin_amdgcn_raw_buffer_load_b128(pr, poff(c, m, n), 0, 16))
                             : acc[m][n];
 #pragma unroll
-    for (int m = 0; m < WR; ++m)
+    for (int m = 0; m < WRW; ++m)
 #pragma unroll
       for (int n = 0; n < NF; ++n) {
         d4 sum = pv[0][m][n];
@@ -993,11 +1009,11 @@ __device__ __forceinline__ void dx3_block(const Dx3Args& g, const Dx3MLArgs* ml)
   const bool lastg = grp == g.ngroup - 1;
   char* xsb = (char*)g.xs;
   // the wave's rows: image, y, pixel, whether the lane has an output there
-  int r_img[WR], r_y[WR];
-  int64_t r_pix[WR];
-  bool r_ok[WR];
+  int r_img[WRW], r_y[WRW];
+  int64_t r_pix[WRW];
+  bool r_ok[WRW];
 #pragma unroll
-  for (int m = 0; m < WR; ++m) {
+  for (int m = 0; m < WRW; ++m) {
     int iy = iyw, y = uyw + m - iyw * g.H;
     if (g.gut) {
       iy = udiv_s(uyw + m, g.hp);
@@ -1010,9 +1026,9 @@ __device__ __forceinline__ void dx3_block(const Dx3Args& g, const Dx3MLArgs* ml)
   }
   // the head's running sums of the wave's rows, loaded before any store of the epilogue (a
   // store may alias them for all the compiler knows, so a load after one would wait it out)
-  d4 hprev[WR];
+  d4 hprev[WRW];
 #pragma unroll
-  for (int m = 0; m < WR; ++m) {
+  for (int m = 0; m < WRW; ++m) {
     hprev[m] = d4{0.f, 0.f, 0.f, 0.f};
     if constexpr (ML) hprev[m] = hreg[m];  // (zeros where the head init left them)
     else if (fh && r_ok[m] && 4 * q < g.nh) hprev[m] = *(const d4*)(g.hacc + r_pix[m] * 16 + 4 * q);
@@ -1020,7 +1036,7 @@ __device__ __forceinline__ void dx3_block(const Dx3Args& g, const Dx3MLArgs* ml)
   // outputs: bias, activation, the fp32 and split stores; acc[m][n] becomes the output (zeros
   // past N), which the head's shares below read
 #pragma unroll
-  for (int m = 0; m < WR; ++m) {
+  for (int m = 0; m < WRW; ++m) {
     const bool row_ok = r_ok[m];
     if (!row_ok && !fh) continue;
     const int cls = bias_class(r_y[m], xj, g.H, g.Wd);
@@ -1070,12 +1086,12 @@ __device__ __forceinline__ void dx3_block(const Dx3Args& g, const Dx3MLArgs* ml)
   }
   if (fh) {
     // this lane's share of the head sums of its pixels (its 4 x NF channels): each head weight
-    // quad read from LDS once and applied to the wave's WR rows (per row and output: channels
+    // quad read from LDS once and applied to the wave's WRW rows (per row and output: channels
     // in order, fragments in order; zero weights past N) -- one read per row cost the epilogue
     // ~8k cycles of LDS bandwidth per block
-    float hp[WR][16];
+    float hp[WRW][16];
 #pragma unroll
-    for (int m = 0; m < WR; ++m)
+    for (int m = 0; m < WRW; ++m)
 #pragma unroll
       for (int o = 0; o < 16; ++o) hp[m][o] = 0.0f;
 #pragma unroll
@@ -1087,14 +1103,14 @@ __device__ __forceinline__ void dx3_block(const Dx3Args& g, const Dx3MLArgs* ml)
         if (o < g.nh) {  // (no early exit: the loop must unroll, hp stays in registers)
           const d4 wv = *(const d4*)(htab + o * (NF * 16) + nl);
 #pragma unroll
-          for (int m = 0; m < WR; ++m)
+          for (int m = 0; m < WRW; ++m)
 #pragma unroll
             for (int k = 0; k < 4; ++k) hp[m][o] = __builtin_fmaf(wv[k], acc[m][n][k], hp[m][o]);
         }
       }
     }
 #pragma unroll
-    for (int m = 0; m < WR; ++m) {
+    for (int m = 0; m < WRW; ++m) {
       // the pixel's 4 lanes (q) reduce-scatter their shares: lane q ends with the sums of head
       // outputs 4q .. 4q + 3 -- (h_q + h_q^2) then + the pair q^1 -- one fixed order per output
       float r8[8], r4[4];
@@ -1163,13 +1179,21 @@ __device__ __forceinline__ void dx3_block(const Dx3Args& g, const Dx3MLArgs* ml)
 
 template <int NF, int WR, int PITCH, int PLANE_KIB, bool BF>
 __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_kernel(Dx3Args g) {
-  dx3_block<NF, WR, PITCH, PLANE_KIB, BF, false>(g, nullptr);
+  __shared__ __attribute__((aligned(16))) char lds[Dx3Lds<NF, WR, PITCH, PLANE_KIB, BF>::BYTES];
+  if constexpr (IDF_DX3_MIX && !BF && WR * kDxWaves == 32 && WR >= 2) {
+    constexpr int D = IDF_DX3_MIX == 2 ? -1 : 1;  // 1: the older waves take WR + 1 rows, 2: WR - 1
+    if (threadIdx.x < 256) dx3_block<NF, WR, PITCH, PLANE_KIB, BF, false, WR + D>(g, nullptr, lds);
+    else dx3_block<NF, WR, PITCH, PLANE_KIB, BF, false, WR - D>(g, nullptr, lds);
+  } else {
+    dx3_block<NF, WR, PITCH, PLANE_KIB, BF, false>(g, nullptr, lds);
+  }
 }
 
 // The fused DenseBlock: every layer of a block, one workgroup per tile (Dx3MLArgs)
 template <int NF, int PITCH, int PLANE_KIB, bool BF>
 __global__ void __launch_bounds__(kDxThreads, 1) conv3_dx3_block_kernel(Dx3Args g, Dx3MLArgs ml) {
-  dx3_block<NF, 16 / kDxWaves, PITCH, PLANE_KIB, BF, true>(g, &ml);
+  __shared__ __attribute__((aligned(16))) char lds[Dx3Lds<NF, 16 / kDxWaves, PITCH, PLANE_KIB, BF>::BYTES];
+  dx3_block<NF, 16 / kDxWaves, PITCH, PLANE_KIB, BF, true>(g, &ml, lds);
 }
 
 // Block-input split: XS channels [c0, c1) of every pixel from the fp32 rows x (ld_x floats),
