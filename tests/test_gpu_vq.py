@@ -212,6 +212,43 @@ def test_vq_argmin_x3_vs_fp64(P, K, D):
     assert int(flag.item()) == 1
 
 
+@pytest.mark.parametrize("P,K,D", [(5, 1, 8), (130, 17, 12), (64, 129, 4)])
+def test_vq_argmin_x3_small_codebooks(P, K, D):
+    """The split-f16 search on codebooks smaller than one 128-code tile (and one past it): one
+    code gives index 0 everywhere; otherwise the index equals the fp32 kernel's wherever a
+    float64 search separates the best two codes by > 1e-3."""
+    from idfcodec import _lib, vq
+    from idfcodec._lib import check, lib, ptr
+    g = torch.Generator().manual_seed(P * K)
+    x = torch.tanh(torch.randn(P, D, generator=g)).cuda()
+    e = torch.randn(K, D, generator=g) * 0.5
+    ex, ys = vq.taps_weights_x3(e.double().numpy().reshape(K, 1, D))
+    ex = torch.from_numpy(ex.reshape(-1)).cuda()
+    e = e.cuda()
+    s = _lib.stream_ptr()
+    en = torch.empty(K, device="cuda")
+    check(lib().idf_vq_norms(s, K, D, ptr(e), D, ptr(en)), "norms")
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    nws = int(lib().idf_vq_argmin_workspace_bytes(P, K))
+    ws = torch.empty(max(nws, 1), dtype=torch.uint8, device="cuda")
+    got = torch.empty(P, dtype=torch.int32, device="cuda")
+    check(lib().idf_vq_argmin_x3_ws(s, P, D, ptr(x), D, ptr(ex), D, ys, K, ptr(en), ptr(got),
+                                    ptr(ws), nws, ptr(flag)), "argmin x3")
+    f32 = torch.empty(P, dtype=torch.int32, device="cuda")
+    check(lib().idf_vq_argmin_ws(s, P, D, ptr(x), D, ptr(e), D, K, ptr(en), ptr(f32), ptr(ws), nws),
+          "argmin")
+    assert int(flag.item()) == 0
+    got, f32 = got.cpu().long(), f32.cpu().long()
+    if K == 1:
+        assert torch.all(got == 0)
+        return
+    xd, ed = x.cpu().double(), e.cpu().double()
+    d = (xd ** 2).sum(1, keepdim=True) + (ed ** 2).sum(1) - 2 * xd @ ed.t()
+    srt, order = torch.sort(d, dim=1, stable=True)
+    ok = (srt[:, 1] - srt[:, 0]) > 1e-3
+    assert torch.equal(got[ok], order[ok, 0]) and torch.equal(got[ok], f32[ok])
+
+
 def test_vq_engine_argmin_modes_agree():
     """VQEngine's split-f16 codebook search (argmin_mode "x3", the default) and the fp32 one give
     the same indices on the reference's encoder data wherever its margin exceeds 1e-4."""
@@ -230,12 +267,15 @@ def test_vq_engine_argmin_modes_agree():
 
 @pytest.mark.parametrize("kind,ci,co,H,W", [("conv4s2", 3, 128, 64, 64), ("conv4s2", 128, 256, 32, 32),
                                             ("conv3", 40, 24, 9, 7), ("conv1", 384, 512, 8, 8),
-                                            ("convT", 384, 256, 8, 8), ("convT", 256, 3, 16, 16)])
+                                            ("convT", 384, 256, 8, 8), ("convT", 256, 3, 16, 16),
+                                            ("conv1", 16, 24, 5, 5), ("conv1", 20, 8, 3, 3),
+                                            ("conv4s2", 20, 36, 10, 10)])
 def test_conv_taps_x3_vs_fp64(kind, ci, co, H, W):
     """idf_conv_taps_x3 (split-f16 products on f16 MFMA) against a float64 conv of the same
     fp32 inputs and weights: within 1e-5 of the output scale and at most 4x the exact-f32
-    kernel's own error; the strided, 3x3, 1x1 and transposed (four parity launches) forms; an
-    input past the f16 pairs' range sets the flag."""
+    kernel's own error; the strided, 3x3, 1x1 and transposed (four parity launches) forms, and
+    k-loops of 1, 2 and 32 chunks (shorter than, and ragged against, the kernel's three chunks
+    in flight); an input past the f16 pairs' range sets the flag."""
     import torch.nn.functional as F
     from idfcodec import _lib, vq
     from idfcodec._lib import check, ptr
